@@ -1,0 +1,195 @@
+/*
+ * zkp.h -- C ABI of the MI355X-native Groth16 prover hot path
+ *          (BLS12-381; G1/G2 Pippenger MSM + radix-2 Fr NTT on gfx950).
+ *
+ * Drop-in boundary for vats98754/zero-knowledge-proofs (Rust, arkworks 0.4):
+ * every entry point below names the reference interface it replaces.  The
+ * Rust-side binding a maintainer would add is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *   - Field elements cross the ABI in CANONICAL (non-Montgomery) form,
+ *     little-endian u64 limbs: Fr = 4 limbs, Fq = 6, Fq2 = c0 then c1.
+ *     (ark's in-memory BigInt layout; Montgomery conversion is internal.)
+ *   - Affine points carry an explicit infinity byte, like ark's
+ *     G1Affine{x, y, infinity}.  x = y = 0 when infinity is set.
+ *   - All host buffers are caller-owned.  A zk_ctx owns its device memory
+ *     and any uploaded proving key; calls on one ctx are serialised by the
+ *     caller; distinct ctxs are independent.  No callbacks, no exceptions.
+ *   - Every function returns a zk_status; zk_last_error() gives detail.
+ */
+#ifndef ZKP_H
+#define ZKP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error kinds map 1:1 onto the reference's error enums:
+ *   GrothError::MSMError            crates/groth16-core/src/lib.rs:75-76,282-283
+ *   GrothError::InvalidWitness      crates/groth16-core/src/lib.rs:63-64,83-98,113-128
+ *   QAPError::PolynomialDivisionFailed crates/groth16-qap/src/lib.rs:76-77,266-268
+ *   QAPError::DomainTooSmall        crates/groth16-qap/src/lib.rs:67-73,101-105
+ *   SetupError::InvalidParams       crates/groth16-setup/src/lib.rs:107-108,128-152 */
+typedef enum {
+  ZK_OK = 0,
+  ZK_ERR_MSM_LEN = 1,
+  ZK_ERR_INVALID_WITNESS = 2,
+  ZK_ERR_QAP_DIVISION = 3,
+  ZK_ERR_DOMAIN = 4,
+  ZK_ERR_SETUP_PARAMS = 5,
+  ZK_ERR_DEVICE = 6,
+  ZK_ERR_RCCL = 7,
+  ZK_ERR_ARG = 8
+} zk_status;
+
+typedef struct { uint64_t l[4]; } zk_fr;                                   /* 32 B  */
+typedef struct { uint64_t x[6], y[6]; uint8_t infinity, _pad[7]; } zk_g1_affine;   /* 104 B */
+typedef struct { uint64_t x[12], y[12]; uint8_t infinity, _pad[7]; } zk_g2_affine; /* 200 B */
+
+/* Proof (crates/groth16-core/src/lib.rs:27-36) */
+typedef struct { zk_g1_affine a; zk_g2_affine b; zk_g1_affine c; } zk_proof;
+
+/* Constraint system in CSR form, rows = constraints.  Replaces the dense
+ * a/b/c_evals matrices of QAP::from_r1cs (crates/groth16-qap/src/lib.rs:114-140)
+ * and the per-variable polynomials of struct QAP (qap:31-46): the same
+ * matrices, never materialised densely.  Columns >= num_variables are
+ * ignored (qap:122-124).  *_val == NULL means every coefficient is 1. */
+typedef struct {
+  uint64_t num_constraints;
+  uint64_t num_variables;
+  const uint64_t *a_rowptr; const uint32_t *a_col; const zk_fr *a_val;
+  const uint64_t *b_rowptr; const uint32_t *b_col; const zk_fr *b_val;
+  const uint64_t *c_rowptr; const uint32_t *c_col; const zk_fr *c_val;
+} zk_r1cs_csr;
+
+/* SetupParams (crates/groth16-setup/src/lib.rs:82-93); tau is the field
+ * the reference calls `s`. */
+typedef struct { zk_fr alpha, beta, gamma, delta, tau; } zk_setup_params;
+
+/* ProvingKey (crates/groth16-setup/src/lib.rs:27-52) minus the embedded
+ * QAP, which is passed as a zk_r1cs_csr.  Arrays are caller-allocated:
+ * a_g1, b_g1, b_g2: num_variables; ic_g1: num_variables - num_public - 1;
+ * h_g1: qap.degree() = domain size n. */
+typedef struct {
+  zk_g1_affine alpha_g1, beta_g1, delta_g1;
+  zk_g2_affine beta_g2, delta_g2;
+  zk_g1_affine *a_g1;  uint64_t a_len;
+  zk_g1_affine *b_g1;  uint64_t b_len;
+  zk_g2_affine *b_g2;  uint64_t b2_len;
+  zk_g1_affine *ic_g1; uint64_t ic_len;
+  zk_g1_affine *h_g1;  uint64_t h_len;
+  uint64_t num_public;
+} zk_pk;
+
+/* VerificationKey (crates/groth16-setup/src/lib.rs:56-69); ic_g1: num_public + 1 */
+typedef struct {
+  zk_g1_affine alpha_g1;
+  zk_g2_affine beta_g2, gamma_g2, delta_g2;
+  zk_g1_affine *ic_g1; uint64_t ic_len;
+  uint64_t num_public;
+} zk_vk;
+
+typedef struct zk_ctx zk_ctx;          /* one GPU, its streams and workspaces */
+typedef struct zk_pk_dev zk_pk_dev;    /* proving key resident in HBM        */
+
+/* ---------------------------------------------------------------- ctx --- */
+/* device: HIP ordinal.  NULL on failure (no GPU, HIP error). */
+zk_ctx *zk_ctx_create(int device);
+void zk_ctx_destroy(zk_ctx *ctx);
+const char *zk_last_error(const zk_ctx *ctx);
+int zk_ctx_synchronize(zk_ctx *ctx);
+
+/* ---------------------------------------------------------------- MSM --- */
+/* Sum_i scalars[i] * bases[i], normalised to affine.  Replaces
+ * Prover::multi_scalar_mult_g1 -> G1Projective::msm (ark-ec 0.4.2
+ * VariableBaseMSM::msm), crates/groth16-core/src/lib.rs:275-286.
+ * nbases != nscalars -> ZK_ERR_MSM_LEN (ark's Err(min_len)).
+ * scalar_bits: 64 when every scalar is < 2^64 (the prove path's lo64
+ * scalars), else 255.  Infinity bases and zero scalars are allowed. */
+int zk_msm_g1(zk_ctx *ctx, const zk_g1_affine *bases, size_t nbases,
+              const zk_fr *scalars, size_t nscalars, uint32_t scalar_bits,
+              zk_g1_affine *out);
+/* Same for G2: crates/groth16-core/src/lib.rs:289-300. */
+int zk_msm_g2(zk_ctx *ctx, const zk_g2_affine *bases, size_t nbases,
+              const zk_fr *scalars, size_t nscalars, uint32_t scalar_bits,
+              zk_g2_affine *out);
+
+/* Device-resident MSM (benchmarks, and callers that keep bases in HBM).
+ * zk_msm_g1_upload converts bases once into the device layout; the scalars
+ * pointer of zk_msm_g1_dev is DEVICE memory holding n canonical zk_fr. */
+typedef struct zk_msm_bases zk_msm_bases;
+int zk_msm_g1_upload(zk_ctx *ctx, const zk_g1_affine *bases, size_t n, zk_msm_bases **out);
+int zk_msm_g2_upload(zk_ctx *ctx, const zk_g2_affine *bases, size_t n, zk_msm_bases **out);
+void zk_msm_bases_free(zk_msm_bases *b);
+int zk_msm_g1_dev(zk_ctx *ctx, const zk_msm_bases *bases, const void *d_scalars, size_t n,
+                  uint32_t scalar_bits, zk_g1_affine *out);
+int zk_msm_g2_dev(zk_ctx *ctx, const zk_msm_bases *bases, const void *d_scalars, size_t n,
+                  uint32_t scalar_bits, zk_g2_affine *out);
+
+/* ---------------------------------------------------------------- NTT --- */
+/* In-place radix-2 transform over Fr of size 2^log_n, natural order in and
+ * out.  Replaces Radix2EvaluationDomain::{fft, ifft, coset_fft, coset_ifft}
+ * (ark-poly 0.4.2) as used at crates/groth16-qap/src/lib.rs:101,167-169,260.
+ * dir: +1 forward (evaluations X_k = sum_j x_j w^jk), -1 inverse (scaled by
+ * n^-1).  coset: NULL, or the shift g (forward evaluates on g*<w>; inverse
+ * undoes it).  log_n <= 32 else ZK_ERR_DOMAIN (Fr 2-adicity is 32). */
+int zk_ntt_fr(zk_ctx *ctx, zk_fr *data, uint32_t log_n, int dir, const zk_fr *coset);
+/* Same on DEVICE memory holding canonical zk_fr. */
+int zk_ntt_fr_dev(zk_ctx *ctx, void *d_data, uint32_t log_n, int dir, const zk_fr *coset);
+
+/* -------------------------------------------------------------- setup --- */
+/* CRS::generate_from_qap (crates/groth16-setup/src/lib.rs:141-268) with the
+ * reference's exact semantics (low-64-bit truncation of every derived scalar,
+ * h_g1 = [lo64(tau~^i / delta~)]_1 for i < n).  Fills caller-allocated pk / vk
+ * arrays (sizes as documented on zk_pk / zk_vk). */
+int zk_groth16_setup(zk_ctx *ctx, const zk_r1cs_csr *qap, const zk_setup_params *params,
+                     uint64_t num_public, zk_pk *pk, zk_vk *vk);
+/* Same, but the proving key stays in HBM (no host round trip); vk may be NULL. */
+int zk_groth16_setup_dev(zk_ctx *ctx, const zk_r1cs_csr *qap, const zk_setup_params *params,
+                         uint64_t num_public, zk_pk_dev **pk_out, zk_vk *vk);
+
+/* -------------------------------------------------------------- prove --- */
+/* Upload a proving key + its constraint system once; it stays resident. */
+int zk_pk_upload(zk_ctx *ctx, const zk_pk *pk, const zk_r1cs_csr *qap, zk_pk_dev **out);
+void zk_pk_free(zk_pk_dev *pk);
+
+/* Prover::prove (crates/groth16-core/src/lib.rs:139-272), bit-exact:
+ * z = full assignment [1 | public | witness] (Witness::assignment), zlen its
+ * length, num_public = Witness::num_public.  r and s are the two Fr::rand
+ * draws of core:152-153, made explicit so proofs are reproducible.
+ * Errors: ZK_ERR_INVALID_WITNESS (Witness::new / validate), ZK_ERR_QAP_DIVISION. */
+int zk_groth16_prove(zk_ctx *ctx, const zk_pk_dev *pk, const zk_fr *z, size_t zlen,
+                     size_t num_public, const zk_fr *r, const zk_fr *s, zk_proof *out);
+/* Same with z in DEVICE memory (zlen canonical zk_fr). */
+int zk_groth16_prove_dev(zk_ctx *ctx, const zk_pk_dev *pk, const void *d_z, size_t zlen,
+                         size_t num_public, const zk_fr *r, const zk_fr *s, zk_proof *out);
+
+/* ---- multi-GPU: MSM sharded by base range (one process per GPU) ---- */
+/* Upload only shard `shard` of `nshards` contiguous ranges of every base
+ * vector (the QAP stays whole: the quotient is replicated per GPU). */
+int zk_pk_upload_shard(zk_ctx *ctx, const zk_pk *pk, const zk_r1cs_csr *qap,
+                       uint32_t shard, uint32_t nshards, zk_pk_dev **out);
+int zk_groth16_setup_dev_shard(zk_ctx *ctx, const zk_r1cs_csr *qap, const zk_setup_params *params,
+                               uint64_t num_public, uint32_t shard, uint32_t nshards,
+                               zk_pk_dev **pk_out);
+/* Opaque per-GPU partial accumulators (Montgomery XYZZ), exchanged by ONE
+ * all-gather over RCCL/xGMI and folded by zk_groth16_prove_combine. */
+#define ZK_PARTIAL_BYTES 1536
+typedef struct { uint8_t bytes[ZK_PARTIAL_BYTES]; } zk_prove_partial;
+int zk_groth16_prove_partial(zk_ctx *ctx, const zk_pk_dev *pk_shard, const void *d_z, size_t zlen,
+                             size_t num_public, const zk_fr *r, const zk_fr *s,
+                             zk_prove_partial *out);
+int zk_groth16_prove_combine(const zk_prove_partial *parts, size_t nparts,
+                             const zk_fr *r, const zk_fr *s, zk_proof *out);
+
+/* ------------------------------------------------------ serialization --- */
+/* ark-serialize CanonicalSerialize, compressed (zcash flag bits), for
+ * Proof (crates/groth16-core/src/lib.rs:28): a(48) | b(96) | c(48). */
+int zk_proof_serialize_compressed(const zk_proof *proof, uint8_t out[192]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZKP_H */

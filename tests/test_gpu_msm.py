@@ -1,0 +1,109 @@
+"""GPU MSM parity (libzkp_amd.so through the C ABI) vs the oracle and the
+golden vectors.  Bit-exact: MSM outputs are unique affine group elements."""
+import numpy as np
+import pytest
+
+from helpers import fr_rows, g1_words, g2_words, golden
+
+pytestmark = pytest.mark.gpu
+G = golden()
+
+
+@pytest.mark.parametrize("vec", G["msm"], ids=lambda v: v["name"])
+def test_msm_golden(ctx, vec):
+    sc = fr_rows(vec["scalars"])
+    bits = 64 if vec["name"].endswith("_64") else 255
+    if vec["group"] == 1:
+        bases = np.array([g1_words(p) for p in vec["bases"]], dtype=np.uint64)
+        assert list(ctx.msm_g1(bases, sc, bits)) == g1_words(vec["out"])
+    else:
+        bases = np.array([g2_words(p) for p in vec["bases"]], dtype=np.uint64)
+        assert list(ctx.msm_g2(bases, sc, bits)) == g2_words(vec["out"])
+
+
+def _g1_bases(oracle, n, seed):
+    g = oracle.g1_generator()
+    ks = oracle.random_fr(n, seed)
+    return np.array([oracle.g1_mul(g, k) for k in oracle.fr_ints(ks)])
+
+
+def _g2_bases(oracle, n, seed):
+    g = oracle.g2_generator()
+    ks = oracle.random_fr(n, seed)
+    return np.array([oracle.g2_mul(g, k & ((1 << 64) - 1)) for k in oracle.fr_ints(ks)])
+
+
+@pytest.fixture(scope="module")
+def g1_pool(oracle):
+    return _g1_bases(oracle, 2048, 11)
+
+
+@pytest.mark.parametrize("n", [1, 2, 31, 100, 1000, 2048])
+@pytest.mark.parametrize("bits", [64, 255])
+def test_msm_g1_random_vs_oracle(ctx, oracle, g1_pool, n, bits):
+    bases = g1_pool[:n].copy()
+    sc = oracle.random_fr(n, 1000 + n)
+    if bits == 64:
+        sc[:, 1:] = 0
+    if n > 4:
+        bases[3] = 0
+        bases[3, 12] = 1            # infinity base
+        sc[4] = 0                    # zero scalar
+    assert np.array_equal(ctx.msm_g1(bases, sc, bits), oracle.msm_g1(bases, sc))
+
+
+def test_msm_g1_degenerate_buckets(ctx, oracle, g1_pool):
+    """Equal points in one bucket (doubling branch), P and -P (cancellation),
+    and one huge bucket spanning many accumulate threads (all scalars 1)."""
+    n = 3000
+    bases = np.repeat(g1_pool[:3], n // 3, axis=0)
+    sc = np.zeros((n, 4), dtype=np.uint64)
+    sc[:, 0] = 1
+    assert np.array_equal(ctx.msm_g1(bases, sc, 64), oracle.msm_g1(bases, sc))
+    # P, -P with equal scalars -> identity
+    p = g1_pool[5].copy()
+    q = oracle.g1_mul(p, oracle.lib and (0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001 - 1))
+    out = ctx.msm_g1(np.array([p, q]), np.array([[7, 0, 0, 0], [7, 0, 0, 0]], dtype=np.uint64), 64)
+    assert out[12] == 1
+    # duplicates with mixed scalars
+    sc = oracle.random_fr(n, 77)
+    sc[:, 1:] = 0
+    sc[:, 0] &= 0xFF                 # few distinct digits: long runs per bucket
+    assert np.array_equal(ctx.msm_g1(bases, sc, 64), oracle.msm_g1(bases, sc))
+
+
+def test_msm_empty_and_len_error(ctx, zkp, g1_pool):
+    out = ctx.msm_g1(np.zeros((0, 13), dtype=np.uint64), np.zeros((0, 4), dtype=np.uint64))
+    assert out[12] == 1
+    with pytest.raises(zkp.MSMError):
+        ctx.msm_g1(g1_pool[:3], np.zeros((2, 4), dtype=np.uint64))
+
+
+@pytest.mark.parametrize("n", [1, 7, 200])
+@pytest.mark.parametrize("bits", [64, 255])
+def test_msm_g2_random_vs_oracle(ctx, oracle, n, bits):
+    bases = _g2_bases(oracle, n, 21 + n)
+    sc = oracle.random_fr(n, 3000 + n)
+    if bits == 64:
+        sc[:, 1:] = 0
+    if n > 4:
+        bases[2] = 0
+        bases[2, 24] = 1
+    assert np.array_equal(ctx.msm_g2(bases, sc, bits), oracle.msm_g2(bases, sc))
+
+
+def test_msm_g1_linearity_large(ctx, oracle):
+    """Size-independent property at 2^16: bases (a + i b) G give
+    G * (a sum s_i + b sum i s_i)."""
+    R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    n, a, b = 1 << 16, 0xDEADBEEF, 0xC0FFEE
+    g = oracle.g1_generator()
+    step = oracle.g1_mul(g, b)
+    bases = np.empty((n, 13), dtype=np.uint64)
+    bases[0] = oracle.g1_mul(g, a)
+    for i in range(1, n):
+        bases[i] = oracle.g1_add(bases[i - 1], step)
+    sc = oracle.random_fr(n, 0x5EED0001)
+    s = oracle.fr_ints(sc)
+    k = (a * sum(s) + b * sum(i * x for i, x in enumerate(s))) % R
+    assert np.array_equal(ctx.msm_g1(bases, sc, 255), oracle.g1_mul(g, k))

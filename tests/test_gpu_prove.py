@@ -1,0 +1,110 @@
+"""Groth16 prove / setup on the GPU: bit-exact against the golden fixtures
+(independent literal restatement) and the C oracle (same pk, z, r, s)."""
+import numpy as np
+import pytest
+
+import gpu_util as U
+from helpers import fr_rows, g1_words, g2_words, golden, proof_words
+
+pytestmark = pytest.mark.gpu
+G = golden()
+
+
+@pytest.mark.parametrize("case", G["prove"], ids=lambda c: c["name"])
+def test_prove_golden(ctx, zkp, case):
+    qap = U.qap_from_case(zkp, case)
+    pk = U.pk_from_golden(zkp, case, qap)
+    dpk = pk.upload(ctx)
+    z = fr_rows(case["z"])
+    r, s = int(case["r"], 16), int(case["s"], 16)
+    w = zkp.Witness(z, case["num_public"])
+    if case["error"] is None:
+        proof = zkp.Prover.prove(dpk, w, r=r, s=s)
+        assert list(proof.words) == proof_words(case)
+        assert proof.serialize_compressed().hex() == case["proof_compressed"]
+    else:
+        exc = zkp.PolynomialDivisionFailed if "QAP" in case["error"] else zkp.InvalidWitness
+        with pytest.raises(exc):
+            zkp.Prover.prove(dpk, w, r=r, s=s)
+
+
+@pytest.mark.parametrize("case", G["prove"], ids=lambda c: c["name"])
+def test_setup_golden(ctx, zkp, case):
+    qap = U.qap_from_case(zkp, case)
+    params = zkp.SetupParams(*[int(x, 16) for x in case["params"]])
+    crs = zkp.CRS.generate_from_qap(ctx, qap, params, case["num_public"])
+    gp = case["pk"]
+    for nm in ("a_g1", "b_g1", "h_g1"):
+        assert np.array_equal(getattr(crs.pk, nm), np.array([g1_words(p) for p in gp[nm]], dtype=np.uint64)), nm
+    if len(gp["ic_g1"]):
+        assert np.array_equal(crs.pk.ic_g1, np.array([g1_words(p) for p in gp["ic_g1"]], dtype=np.uint64))
+    assert np.array_equal(crs.pk.b_g2, np.array([g2_words(p) for p in gp["b_g2"]], dtype=np.uint64))
+    for nm in ("alpha_g1", "beta_g1", "delta_g1"):
+        assert list(crs.pk.point(nm)) == g1_words(gp[nm])
+    for nm in ("beta_g2", "delta_g2"):
+        assert list(crs.pk.point(nm)) == g2_words(gp[nm])
+    assert list(crs.vk.point("gamma_g2")) == g2_words(case["vk"]["gamma_g2"])
+    assert np.array_equal(crs.vk.ic_g1, np.array([g1_words(p) for p in case["vk"]["ic_g1"]], dtype=np.uint64))
+
+
+def _synthetic(zkp, oracle, log_n, seed):
+    n = 1 << log_n
+    qap = zkp.QAP(zkp.CSRMatrices.synthetic(n))
+    csr_o = oracle.CSR.synthetic(n)
+    rng = __import__("pyref").SplitMix64(seed)
+    params = [rng.fr() for _ in range(5)]
+    r, s = rng.fr(), rng.fr()
+    z = oracle.synthetic_witness(n, seed + 1)
+    return qap, csr_o, params, r, s, z
+
+
+@pytest.mark.parametrize("log_n", [6, 10, 12])
+def test_prove_synthetic_vs_oracle(ctx, zkp, oracle, log_n):
+    qap, csr_o, params, r, s, z = _synthetic(zkp, oracle, log_n, 100 + log_n)
+    rc, opk, _ = oracle.setup(csr_o, params, 1, nthreads=8)
+    assert rc == 0
+    rc, oproof = oracle.prove(opk, csr_o, z, 1, r, s)
+    assert rc == 0
+    dpk = U.pk_from_oracle(zkp, opk, qap, 1).upload(ctx)
+    proof = zkp.Prover.prove(dpk, zkp.Witness(z, 1), r=r, s=s)
+    assert np.array_equal(proof.words, oproof)
+    # GPU setup straight into HBM gives the same proof
+    dpk2 = zkp.CRS.generate_device(ctx, qap, zkp.SetupParams(*params), 1)
+    proof2 = zkp.Prover.prove(dpk2, zkp.Witness(z, 1), r=r, s=s)
+    assert np.array_equal(proof2.words, oproof)
+
+
+def test_setup_synthetic_vs_oracle(ctx, zkp, oracle):
+    qap, csr_o, params, r, s, z = _synthetic(zkp, oracle, 10, 555)
+    rc, opk, ovk = oracle.setup(csr_o, params, 1, nthreads=8)
+    crs = zkp.CRS.generate_from_qap(ctx, qap, zkp.SetupParams(*params), 1)
+    for nm in ("a_g1", "b_g1", "b_g2", "h_g1"):
+        assert np.array_equal(getattr(crs.pk, nm), getattr(opk, nm)), nm
+    assert np.array_equal(crs.pk.ic_g1, opk.ic_g1[:len(crs.pk.ic_g1)])
+    assert np.array_equal(crs.vk.ic_g1, ovk.ic_g1)
+
+
+@pytest.mark.parametrize("nshards", [2, 3])
+def test_sharded_prove_equals_full(ctx, zkp, oracle, nshards):
+    """MSM sharded by base range + one gather + fold == single-GPU proof
+    (the multi-GPU path of SURVEY 8(e), emulated on one device)."""
+    import ctypes as C
+    qap, csr_o, params, r, s, z = _synthetic(zkp, oracle, 9, 900 + nshards)
+    rc, opk, _ = oracle.setup(csr_o, params, 1, nthreads=8)
+    rc, oproof = oracle.prove(opk, csr_o, z, 1, r, s)
+    pk = U.pk_from_oracle(zkp, opk, qap, 1)
+    import torch
+    dz = torch.from_numpy(z.view(np.int64).copy()).cuda()
+    parts = []
+    for k in range(nshards):
+        dpk = pk.upload(ctx, shard=k, nshards=nshards)
+        parts.append(zkp.Prover.prove_partial(dpk, dz.data_ptr(), len(z), 1, r, s))
+        torch.cuda.synchronize()
+    proof = zkp.Prover.combine(parts, r, s)
+    assert np.array_equal(proof.words, oproof)
+    # setup-side sharding too
+    parts = []
+    for k in range(nshards):
+        dpk = zkp.CRS.generate_device(ctx, qap, zkp.SetupParams(*params), 1, shard=k, nshards=nshards)
+        parts.append(zkp.Prover.prove_partial(dpk, dz.data_ptr(), len(z), 1, r, s))
+    assert np.array_equal(zkp.Prover.combine(parts, r, s).words, oproof)

@@ -1,0 +1,637 @@
+"""zero-knowledge-proofs_amd -- MI355X-native Groth16 prover hot path.
+
+Python mirror of the reference's prover/setup interface (vats98754/
+zero-knowledge-proofs, Rust) over the C ABI of include/zkp.h, which is
+implemented by libzkp_amd.so (hand-written gfx950 HIP kernels).  Names,
+argument meaning and error behaviour follow the reference crates:
+
+  R1CS / LinearCombination / Variable  crates/groth16-r1cs/src/lib.rs:16-358
+  QAP.from_r1cs / degree               crates/groth16-qap/src/lib.rs:95-187, 285-294
+  SetupParams / CRS.generate_from_qap  crates/groth16-setup/src/lib.rs:82-278
+  Witness / Prover.prove / Proof       crates/groth16-core/src/lib.rs:27-272
+  GrothError kinds                     crates/groth16-core/src/lib.rs:47-77
+
+There is no CPU fallback: every compute call goes through libzkp_amd.so on a
+GPU, and loading fails loudly when the library (or a GPU) is missing.
+The package directory name contains hyphens; import it with
+importlib.import_module("zero-knowledge-proofs_amd").
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libzkp_amd.so")
+
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001  # Fr modulus
+
+ZK_OK, ZK_ERR_MSM_LEN, ZK_ERR_INVALID_WITNESS, ZK_ERR_QAP_DIVISION, ZK_ERR_DOMAIN, \
+    ZK_ERR_SETUP_PARAMS, ZK_ERR_DEVICE, ZK_ERR_RCCL, ZK_ERR_ARG = range(9)
+G1_WORDS, G2_WORDS = 13, 25
+PARTIAL_BYTES = 1536
+
+# C-ABI symbols declared in include/zkp.h (checked by tests/test_capi.py)
+EXPORTS = (
+    "zk_ctx_create", "zk_ctx_destroy", "zk_last_error", "zk_ctx_synchronize",
+    "zk_msm_g1", "zk_msm_g2", "zk_msm_g1_upload", "zk_msm_g2_upload", "zk_msm_bases_free",
+    "zk_msm_g1_dev", "zk_msm_g2_dev", "zk_ntt_fr", "zk_ntt_fr_dev",
+    "zk_groth16_setup", "zk_groth16_setup_dev", "zk_pk_upload", "zk_pk_free",
+    "zk_groth16_prove", "zk_groth16_prove_dev", "zk_pk_upload_shard",
+    "zk_groth16_setup_dev_shard", "zk_groth16_prove_partial", "zk_groth16_prove_combine",
+    "zk_proof_serialize_compressed",
+)
+
+
+# ------------------------------------------------------------- errors ----
+class GrothError(Exception):
+    """crates/groth16-core/src/lib.rs:47-77"""
+
+
+class InvalidWitness(GrothError):
+    pass
+
+
+class MSMError(GrothError):
+    pass
+
+
+class QAPError(GrothError):
+    """crates/groth16-qap/src/lib.rs:63-86"""
+
+
+class PolynomialDivisionFailed(QAPError):
+    pass
+
+
+class DomainTooSmall(QAPError):
+    pass
+
+
+class SetupError(GrothError):
+    """crates/groth16-setup/src/lib.rs:95-113 (InvalidParams)"""
+
+
+class DeviceError(GrothError):
+    pass
+
+
+_STATUS = {ZK_ERR_MSM_LEN: MSMError, ZK_ERR_INVALID_WITNESS: InvalidWitness,
+           ZK_ERR_QAP_DIVISION: PolynomialDivisionFailed, ZK_ERR_DOMAIN: DomainTooSmall,
+           ZK_ERR_SETUP_PARAMS: SetupError, ZK_ERR_DEVICE: DeviceError,
+           ZK_ERR_RCCL: DeviceError, ZK_ERR_ARG: ValueError}
+
+
+# ---------------------------------------------------------- C structs ----
+class _Fr(C.Structure):
+    _fields_ = [("l", C.c_uint64 * 4)]
+
+
+class _G1(C.Structure):
+    _fields_ = [("w", C.c_uint64 * G1_WORDS)]
+
+
+class _G2(C.Structure):
+    _fields_ = [("w", C.c_uint64 * G2_WORDS)]
+
+
+class _Proof(C.Structure):
+    _fields_ = [("a", _G1), ("b", _G2), ("c", _G1)]
+
+
+class _CSR(C.Structure):
+    _fields_ = [("num_constraints", C.c_uint64), ("num_variables", C.c_uint64)] + [
+        (f"{m}_{f}", C.c_void_p) for m in "abc" for f in ("rowptr", "col", "val")]
+
+
+class _SetupParams(C.Structure):
+    _fields_ = [(k, _Fr) for k in ("alpha", "beta", "gamma", "delta", "tau")]
+
+
+class _PK(C.Structure):
+    _fields_ = [("alpha_g1", _G1), ("beta_g1", _G1), ("delta_g1", _G1),
+                ("beta_g2", _G2), ("delta_g2", _G2),
+                ("a_g1", C.c_void_p), ("a_len", C.c_uint64),
+                ("b_g1", C.c_void_p), ("b_len", C.c_uint64),
+                ("b_g2", C.c_void_p), ("b2_len", C.c_uint64),
+                ("ic_g1", C.c_void_p), ("ic_len", C.c_uint64),
+                ("h_g1", C.c_void_p), ("h_len", C.c_uint64),
+                ("num_public", C.c_uint64)]
+
+
+class _VK(C.Structure):
+    _fields_ = [("alpha_g1", _G1), ("beta_g2", _G2), ("gamma_g2", _G2), ("delta_g2", _G2),
+                ("ic_g1", C.c_void_p), ("ic_len", C.c_uint64), ("num_public", C.c_uint64)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libzkp_amd.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `make -C zero-knowledge-proofs_amd/csrc`")
+        # One HIP runtime per process: torch bundles its own libamdhip64
+        # (SONAME libamdhip64.so.7).  Loading torch first makes our DT_NEEDED
+        # bind to that copy, so torch device memory, streams and RCCL
+        # (torch.distributed) share the runtime with our kernels.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        L = C.CDLL(LIB_PATH)
+        L.zk_ctx_create.restype = C.c_void_p
+        L.zk_ctx_create.argtypes = [C.c_int]
+        L.zk_ctx_destroy.argtypes = [C.c_void_p]
+        L.zk_last_error.restype = C.c_char_p
+        L.zk_last_error.argtypes = [C.c_void_p]
+        for name in EXPORTS:
+            f = getattr(L, name)
+            if name not in ("zk_ctx_create", "zk_ctx_destroy", "zk_last_error",
+                            "zk_msm_bases_free", "zk_pk_free"):
+                f.restype = C.c_int
+        L.zk_msm_bases_free.argtypes = [C.c_void_p]
+        L.zk_pk_free.argtypes = [C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return C.c_void_p(a.ctypes.data)
+
+
+def _check(rc, ctx=None, what=""):
+    if rc == ZK_OK:
+        return
+    detail = ""
+    if ctx is not None:
+        msg = lib().zk_last_error(ctx._h)
+        detail = msg.decode() if msg else ""
+    raise _STATUS.get(rc, GrothError)(f"{what} failed ({rc}) {detail}".strip())
+
+
+# ------------------------------------------------------------ helpers ----
+def to_limbs(v, k=4):
+    v = int(v)
+    return [(v >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(k)]
+
+
+def from_limbs(a):
+    return sum(int(x) << (64 * i) for i, x in enumerate(np.asarray(a).reshape(-1)))
+
+
+def fr_array(values):
+    """ints (reduced mod r) -> (n, 4) uint64 canonical limbs."""
+    values = [int(v) % R for v in values]
+    out = np.zeros((len(values), 4), dtype=np.uint64)
+    for i, v in enumerate(values):
+        out[i] = to_limbs(v)
+    return out
+
+
+def _fr(v):
+    f = _Fr()
+    for i, x in enumerate(to_limbs(int(v) % R)):
+        f.l[i] = x
+    return f
+
+
+# ------------------------------------------------------------ context ----
+class Context:
+    """One GPU (zk_ctx): streams, cached NTT domains, MSM workspaces."""
+
+    def __init__(self, device=0):
+        self._h = lib().zk_ctx_create(int(device))
+        if not self._h:
+            raise DeviceError(f"zk_ctx_create({device}) failed: no usable GPU")
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().zk_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- MSM (crates/groth16-core/src/lib.rs:275-300) ----
+    def msm_g1(self, bases, scalars, scalar_bits=255):
+        """bases: (n, 13) uint64 canonical affine; scalars: (n, 4) uint64 canonical Fr."""
+        bases = np.ascontiguousarray(bases, dtype=np.uint64).reshape(-1, G1_WORDS)
+        scalars = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1, 4)
+        out = np.zeros(G1_WORDS, dtype=np.uint64)
+        rc = lib().zk_msm_g1(C.c_void_p(self._h), _p(bases), C.c_size_t(len(bases)), _p(scalars),
+                             C.c_size_t(len(scalars)), C.c_uint32(scalar_bits), _p(out))
+        _check(rc, self, "zk_msm_g1")
+        return out
+
+    def msm_g2(self, bases, scalars, scalar_bits=255):
+        bases = np.ascontiguousarray(bases, dtype=np.uint64).reshape(-1, G2_WORDS)
+        scalars = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1, 4)
+        out = np.zeros(G2_WORDS, dtype=np.uint64)
+        rc = lib().zk_msm_g2(C.c_void_p(self._h), _p(bases), C.c_size_t(len(bases)), _p(scalars),
+                             C.c_size_t(len(scalars)), C.c_uint32(scalar_bits), _p(out))
+        _check(rc, self, "zk_msm_g2")
+        return out
+
+    # ---- NTT (ark-poly Radix2EvaluationDomain fft / ifft / coset) ----
+    def ntt(self, data, inverse=False, coset=None):
+        a = np.ascontiguousarray(data, dtype=np.uint64).reshape(-1, 4).copy()
+        n = len(a)
+        log_n = n.bit_length() - 1
+        if n == 0 or (1 << log_n) != n:
+            raise DomainTooSmall(f"NTT size {n} is not a power of two")
+        g = C.byref(_fr(coset)) if coset is not None else None
+        rc = lib().zk_ntt_fr(C.c_void_p(self._h), _p(a), C.c_uint32(log_n),
+                             C.c_int(-1 if inverse else 1), g)
+        _check(rc, self, "zk_ntt_fr")
+        return a
+
+
+# --------------------------------------------------------------- R1CS ----
+class Variable(int):
+    """crates/groth16-r1cs/src/lib.rs:20-35; Variable.ONE = 0."""
+
+    def index(self):
+        return int(self)
+
+
+Variable.ONE = Variable(0)
+
+
+class LinearCombination:
+    """Sparse sum of coeff * var (crates/groth16-r1cs/src/lib.rs:46-118)."""
+
+    def __init__(self, terms=None):
+        self.terms = {}
+        for v, c in (terms or {}).items():
+            self.add_term(v, c)
+
+    @classmethod
+    def from_variable(cls, var):
+        return cls({Variable(var): 1})
+
+    @classmethod
+    def from_constant(cls, c):
+        return cls({Variable.ONE: c} if int(c) % R else {})
+
+    def add_term(self, var, coeff):
+        coeff = int(coeff) % R
+        if coeff == 0:
+            return
+        var = Variable(var)
+        v = (self.terms.get(var, 0) + coeff) % R
+        if v:
+            self.terms[var] = v
+        else:
+            self.terms.pop(var, None)
+
+    def sub_lc(self, other):
+        for v, c in other.terms.items():
+            self.add_term(v, -c)
+
+
+class R1CS:
+    """crates/groth16-r1cs/src/lib.rs:229-358 (the builder subset on the path)."""
+
+    def __init__(self, num_public_inputs=0):
+        self.constraints = []
+        self.num_public_inputs = num_public_inputs
+        self.num_variables = 1 + num_public_inputs
+
+    def allocate_variable(self):
+        v = Variable(self.num_variables)
+        self.num_variables += 1
+        return v
+
+    def add_constraint(self, a, b, c):
+        self.constraints.append((a, b, c))
+
+    def enforce_multiplication(self, a, b, c):
+        self.add_constraint(a, b, c)
+
+    def enforce_equal(self, left, right):
+        diff = LinearCombination(dict(left.terms))
+        diff.sub_lc(right)
+        self.add_constraint(diff, LinearCombination.from_constant(1), LinearCombination())
+
+    def num_constraints(self):
+        return len(self.constraints)
+
+    def is_satisfied(self, z):
+        z = [int(x) % R for x in z]
+        for a, b, c in self.constraints:
+            ev = [sum(z[v] * k for v, k in lc.terms.items() if v < len(z)) % R for lc in (a, b, c)]
+            if ev[0] * ev[1] % R != ev[2]:
+                return False
+        return True
+
+
+class CSRMatrices:
+    """The constraint matrices in CSR (zk_r1cs_csr); keeps the buffers alive."""
+
+    def __init__(self, num_constraints, num_variables, mats):
+        self.num_constraints, self.num_variables = int(num_constraints), int(num_variables)
+        self.mats = mats  # 3 x (rowptr u64[nc+1], col u32[nnz], val u64[nnz,4] or None)
+        self.s = _CSR()
+        self.s.num_constraints, self.s.num_variables = self.num_constraints, self.num_variables
+        for m, (rp, col, val) in zip("abc", mats):
+            setattr(self.s, f"{m}_rowptr", rp.ctypes.data)
+            setattr(self.s, f"{m}_col", col.ctypes.data)
+            setattr(self.s, f"{m}_val", val.ctypes.data if val is not None else None)
+
+    @classmethod
+    def from_r1cs(cls, cs):
+        mats = []
+        for m in range(3):
+            rp, cols, vals = [0], [], []
+            for con in cs.constraints:
+                for var in sorted(con[m].terms):
+                    cols.append(int(var))
+                    vals.append(to_limbs(con[m].terms[var]))
+                rp.append(len(cols))
+            mats.append((np.array(rp, dtype=np.uint64), np.array(cols, dtype=np.uint32),
+                         np.array(vals, dtype=np.uint64).reshape(-1, 4)))
+        return cls(cs.num_constraints(), cs.num_variables, mats)
+
+    @classmethod
+    def synthetic(cls, n):
+        """groth16-cli generate_crs circuit (crates/groth16-cli/src/lib.rs:57-70):
+        n x (x_j * y_j = z_j), variables x_j = 1+3j, y_j = 2+3j, z_j = 3+3j,
+        unit coefficients (val = NULL)."""
+        rp = np.arange(n + 1, dtype=np.uint64)
+        j = np.arange(n, dtype=np.uint32)
+        mats = [(rp, (1 + 3 * j).astype(np.uint32), None), (rp, (2 + 3 * j).astype(np.uint32), None),
+                (rp, (3 + 3 * j).astype(np.uint32), None)]
+        return cls(n, 3 * n + 1, mats)
+
+
+class QAP:
+    """crates/groth16-qap/src/lib.rs:31-46 in sparse form: the constraint
+    matrices plus the radix-2 domain; the per-variable polynomials of the
+    reference are never materialised (they are implied by the matrices)."""
+
+    def __init__(self, csr):
+        self.csr = csr
+        self.num_variables = csr.num_variables
+        self.num_constraints = csr.num_constraints
+        n = 1
+        while n < self.num_constraints:
+            n <<= 1
+        if n.bit_length() - 1 > 32:
+            raise DomainTooSmall(f"domain {n} exceeds 2^32")
+        self.domain_size = n
+
+    @classmethod
+    def from_r1cs(cls, cs):
+        return cls(CSRMatrices.from_r1cs(cs))
+
+    def degree(self):
+        """max(per-variable degree < n, deg Z = n) = n (qap:285-294)."""
+        return self.domain_size
+
+
+# -------------------------------------------------------------- setup ----
+class SetupParams:
+    """crates/groth16-setup/src/lib.rs:82-136 (`s` is tau)."""
+
+    def __init__(self, alpha, beta, gamma, delta, s):
+        self.alpha, self.beta, self.gamma, self.delta, self.s = (int(x) % R for x in (alpha, beta, gamma, delta, s))
+
+    @classmethod
+    def random(cls, rng):
+        """rng: callable returning a uniform Fr int (e.g. SplitMix64.fr)."""
+        return cls(rng(), rng(), rng(), rng(), rng())
+
+    def validate(self):
+        if 0 in (self.alpha, self.beta, self.gamma, self.delta):
+            raise SetupError("Setup parameters must be non-zero")
+
+    def _c(self):
+        p = _SetupParams()
+        for k, v in (("alpha", self.alpha), ("beta", self.beta), ("gamma", self.gamma),
+                     ("delta", self.delta), ("tau", self.s)):
+            setattr(p, k, _fr(v))
+        return p
+
+
+class ProvingKey:
+    """crates/groth16-setup/src/lib.rs:27-52 (host arrays, canonical affine)."""
+
+    def __init__(self, V, n, num_public, qap):
+        self.a_g1 = np.zeros((V, G1_WORDS), dtype=np.uint64)
+        self.b_g1 = np.zeros((V, G1_WORDS), dtype=np.uint64)
+        self.b_g2 = np.zeros((V, G2_WORDS), dtype=np.uint64)
+        self.ic_g1 = np.zeros((max(V - num_public - 1, 0), G1_WORDS), dtype=np.uint64)
+        self.h_g1 = np.zeros((n, G1_WORDS), dtype=np.uint64)
+        self.num_public = num_public
+        self.qap = qap
+        self.s = _PK()
+
+    def _bind(self):
+        s = self.s
+        s.a_g1, s.a_len = self.a_g1.ctypes.data, len(self.a_g1)
+        s.b_g1, s.b_len = self.b_g1.ctypes.data, len(self.b_g1)
+        s.b_g2, s.b2_len = self.b_g2.ctypes.data, len(self.b_g2)
+        s.ic_g1, s.ic_len = (self.ic_g1.ctypes.data if len(self.ic_g1) else None), len(self.ic_g1)
+        s.h_g1, s.h_len = self.h_g1.ctypes.data, len(self.h_g1)
+        s.num_public = self.num_public
+        return s
+
+    def point(self, name):
+        """alpha_g1 / beta_g1 / delta_g1 / beta_g2 / delta_g2 as uint64 words."""
+        return np.array(getattr(self.s, name).w, dtype=np.uint64)
+
+    def upload(self, ctx, shard=0, nshards=1):
+        return DeviceProvingKey.upload(ctx, self, shard, nshards)
+
+
+class VerificationKey:
+    """crates/groth16-setup/src/lib.rs:56-69"""
+
+    def __init__(self, num_public):
+        self.ic_g1 = np.zeros((num_public + 1, G1_WORDS), dtype=np.uint64)
+        self.num_public = num_public
+        self.s = _VK()
+        self.s.ic_g1 = self.ic_g1.ctypes.data
+
+    def point(self, name):
+        return np.array(getattr(self.s, name).w, dtype=np.uint64)
+
+
+class DeviceProvingKey:
+    """A proving key resident in HBM (zk_pk_dev)."""
+
+    def __init__(self, ctx, handle, qap):
+        self.ctx, self._h, self.qap = ctx, handle, qap
+
+    @classmethod
+    def upload(cls, ctx, pk, shard=0, nshards=1):
+        h = C.c_void_p()
+        s = pk._bind()
+        if nshards == 1:
+            rc = lib().zk_pk_upload(C.c_void_p(ctx._h), C.byref(s), C.byref(pk.qap.csr.s), C.byref(h))
+        else:
+            rc = lib().zk_pk_upload_shard(C.c_void_p(ctx._h), C.byref(s), C.byref(pk.qap.csr.s),
+                                          C.c_uint32(shard), C.c_uint32(nshards), C.byref(h))
+        _check(rc, ctx, "zk_pk_upload")
+        return cls(ctx, h.value, pk.qap)
+
+    def free(self):
+        if getattr(self, "_h", None):
+            lib().zk_pk_free(C.c_void_p(self._h))
+            self._h = None
+
+    def __del__(self):
+        self.free()
+
+
+class CRS:
+    """crates/groth16-setup/src/lib.rs:72-78, 139-278 (GPU setup)."""
+
+    def __init__(self, pk, vk):
+        self.pk, self.vk = pk, vk
+
+    @classmethod
+    def generate_from_qap(cls, ctx, qap, params, num_public):
+        params.validate()
+        if num_public >= qap.num_variables:
+            raise SetupError("Number of public inputs must be less than total variables")
+        pk = ProvingKey(qap.num_variables, qap.domain_size, num_public, qap)
+        vk = VerificationKey(num_public)
+        s = pk._bind()
+        rc = lib().zk_groth16_setup(C.c_void_p(ctx._h), C.byref(qap.csr.s), C.byref(params._c()),
+                                    C.c_uint64(num_public), C.byref(s), C.byref(vk.s))
+        _check(rc, ctx, "zk_groth16_setup")
+        return cls(pk, vk)
+
+    @classmethod
+    def generate_random(cls, ctx, qap, num_public, rng):
+        return cls.generate_from_qap(ctx, qap, SetupParams.random(rng), num_public)
+
+    @staticmethod
+    def generate_device(ctx, qap, params, num_public, shard=0, nshards=1):
+        """Setup straight into HBM (no host round trip) -> DeviceProvingKey."""
+        h = C.c_void_p()
+        if nshards == 1:
+            rc = lib().zk_groth16_setup_dev(C.c_void_p(ctx._h), C.byref(qap.csr.s), C.byref(params._c()),
+                                            C.c_uint64(num_public), C.byref(h), None)
+        else:
+            rc = lib().zk_groth16_setup_dev_shard(C.c_void_p(ctx._h), C.byref(qap.csr.s),
+                                                  C.byref(params._c()), C.c_uint64(num_public),
+                                                  C.c_uint32(shard), C.c_uint32(nshards), C.byref(h))
+        _check(rc, ctx, "zk_groth16_setup_dev")
+        return DeviceProvingKey(ctx, h.value, qap)
+
+
+# -------------------------------------------------------------- prove ----
+class Witness:
+    """crates/groth16-core/src/lib.rs:40-131"""
+
+    def __init__(self, assignment, num_public):
+        a = assignment
+        if not isinstance(a, np.ndarray):
+            a = fr_array(a)
+        a = np.ascontiguousarray(a, dtype=np.uint64).reshape(-1, 4)
+        if num_public >= len(a):
+            raise InvalidWitness("Number of public inputs must be less than total assignment length")
+        if len(a) == 0 or not (a[0, 0] == 1 and not a[0, 1:].any()):
+            raise InvalidWitness("First element of assignment must be 1 (constant)")
+        self.assignment = a
+        self.num_public = num_public
+
+    def public_inputs(self):
+        return self.assignment[1:self.num_public + 1]
+
+
+class Proof:
+    """crates/groth16-core/src/lib.rs:27-36 (a: G1, b: G2, c: G1)."""
+
+    def __init__(self, words):
+        self.words = np.asarray(words, dtype=np.uint64).reshape(-1)
+        self.a = self.words[:G1_WORDS]
+        self.b = self.words[G1_WORDS:G1_WORDS + G2_WORDS]
+        self.c = self.words[G1_WORDS + G2_WORDS:]
+
+    @classmethod
+    def _from_c(cls, p):
+        return cls(list(p.a.w) + list(p.b.w) + list(p.c.w))
+
+    def _c(self):
+        p = _Proof()
+        for i in range(G1_WORDS):
+            p.a.w[i] = int(self.a[i])
+            p.c.w[i] = int(self.c[i])
+        for i in range(G2_WORDS):
+            p.b.w[i] = int(self.b[i])
+        return p
+
+    def serialize_compressed(self):
+        """ark CanonicalSerialize (compressed) of Proof: 48 + 96 + 48 bytes."""
+        out = (C.c_uint8 * 192)()
+        _check(lib().zk_proof_serialize_compressed(C.byref(self._c()), out), None, "serialize")
+        return bytes(out)
+
+    def __eq__(self, other):
+        return isinstance(other, Proof) and np.array_equal(self.words, other.words)
+
+
+class Prover:
+    """Prover::prove (crates/groth16-core/src/lib.rs:139-272).  `r` and `s`
+    are the two Fr::rand draws of core:152-153; pass them explicitly (or an
+    `rng` callable returning Fr ints, drawn r then s)."""
+
+    @staticmethod
+    def prove(dpk, witness, r=None, s=None, rng=None):
+        if r is None or s is None:
+            if rng is None:
+                raise ValueError("pass r and s, or an rng")
+            r, s = rng(), rng()
+        ctx = dpk.ctx
+        out = _Proof()
+        z = witness.assignment
+        rc = lib().zk_groth16_prove(C.c_void_p(ctx._h), C.c_void_p(dpk._h), _p(z), C.c_size_t(len(z)),
+                                    C.c_size_t(witness.num_public), C.byref(_fr(r)), C.byref(_fr(s)),
+                                    C.byref(out))
+        _check(rc, ctx, "zk_groth16_prove")
+        return Proof._from_c(out)
+
+    @staticmethod
+    def prove_device(dpk, d_z_ptr, zlen, num_public, r, s):
+        """z already in HBM (canonical zk_fr array at device pointer d_z_ptr)."""
+        ctx = dpk.ctx
+        out = _Proof()
+        rc = lib().zk_groth16_prove_dev(C.c_void_p(ctx._h), C.c_void_p(dpk._h), C.c_void_p(d_z_ptr),
+                                        C.c_size_t(zlen), C.c_size_t(num_public), C.byref(_fr(r)),
+                                        C.byref(_fr(s)), C.byref(out))
+        _check(rc, ctx, "zk_groth16_prove_dev")
+        return Proof._from_c(out)
+
+    @staticmethod
+    def prove_partial(dpk, d_z_ptr, zlen, num_public, r, s):
+        """This GPU's shard of the MSMs -> opaque bytes for the all-gather."""
+        ctx = dpk.ctx
+        buf = (C.c_uint8 * PARTIAL_BYTES)()
+        rc = lib().zk_groth16_prove_partial(C.c_void_p(ctx._h), C.c_void_p(dpk._h), C.c_void_p(d_z_ptr),
+                                            C.c_size_t(zlen), C.c_size_t(num_public), C.byref(_fr(r)),
+                                            C.byref(_fr(s)), buf)
+        _check(rc, ctx, "zk_groth16_prove_partial")
+        return bytes(buf)
+
+    @staticmethod
+    def combine(partials, r, s):
+        k = len(partials)
+        arr = (C.c_uint8 * (PARTIAL_BYTES * k)).from_buffer_copy(b"".join(partials))
+        out = _Proof()
+        rc = lib().zk_groth16_prove_combine(arr, C.c_size_t(k), C.byref(_fr(r)), C.byref(_fr(s)),
+                                            C.byref(out))
+        _check(rc, None, "zk_groth16_prove_combine")
+        return Proof._from_c(out)

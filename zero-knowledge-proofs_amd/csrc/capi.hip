@@ -1,0 +1,338 @@
+// capi.hip -- extern "C" boundary (include/zkp.h).  Every entry point catches
+// zk::Error / std::exception and returns a zk_status; nothing throws across.
+#include <cstring>
+#include <vector>
+
+#include "ctx.hpp"
+
+namespace zk {
+zk_pk_dev* pk_upload(zk_ctx* ctx, const zk_pk* pk, const zk_r1cs_csr* q, uint32_t shard, uint32_t nshards);
+int prove_impl(zk_ctx*, const zk_pk_dev*, const void*, size_t, size_t, const zk_fr*, const zk_fr*, zk_proof*);
+int prove_partial_impl(zk_ctx*, const zk_pk_dev*, const void*, size_t, size_t, const zk_fr*, const zk_fr*,
+                       zk_prove_partial*);
+int combine_impl(const zk_prove_partial*, size_t, const zk_fr*, const zk_fr*, zk_proof*);
+int setup_impl(zk_ctx*, const zk_r1cs_csr*, const zk_setup_params*, uint64_t, uint32_t, uint32_t, zk_pk*,
+               zk_pk_dev**, zk_vk*);
+void serialize_g1_compressed(const zk_g1_affine& p, uint8_t* out);
+void serialize_g2_compressed(const zk_g2_affine& p, uint8_t* out);
+}  // namespace zk
+
+using namespace zk;
+
+NttDomain& zk_ctx::domain(uint32_t log_n) {
+  auto it = domains.find(log_n);
+  if (it != domains.end()) return *it->second;
+  std::unique_ptr<NttDomain> d(new NttDomain());
+  ntt_domain_init(*d, log_n, stream);
+  NttDomain& ref = *d;
+  domains[log_n] = std::move(d);
+  return ref;
+}
+
+#define ZK_GUARD(ctx, ...)                                    \
+  try {                                                       \
+    if (ctx) ZK_HIP(hipSetDevice((ctx)->device));             \
+    __VA_ARGS__                                               \
+  } catch (const zk::Error& e) {                              \
+    if (ctx) (ctx)->err = e.what();                           \
+    return e.code;                                            \
+  } catch (const std::exception& e) {                         \
+    if (ctx) (ctx)->err = e.what();                           \
+    return ZK_ERR_DEVICE;                                     \
+  }
+
+// Definitions below inherit C linkage from their declarations in include/zkp.h.
+
+zk_ctx* zk_ctx_create(int device) {
+  try {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return nullptr;
+    ZK_HIP(hipSetDevice(device));
+    std::unique_ptr<zk_ctx> c(new zk_ctx());
+    c->device = device;
+    ZK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (int i = 0; i < NUM_MSM; i++) ZK_HIP(hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking));
+    ZK_HIP(hipEventCreateWithFlags(&c->ev_quot, hipEventDisableTiming));
+    ZK_HIP(hipEventCreateWithFlags(&c->ev_scal, hipEventDisableTiming));
+    return c.release();
+  } catch (...) {
+    return nullptr;
+  }
+}
+
+void zk_ctx_destroy(zk_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (int i = 0; i < NUM_MSM; i++) (void)hipStreamSynchronize(ctx->side[i]);
+  ctx->domains.clear();
+  for (int i = 0; i < NUM_MSM; i++) (void)hipStreamDestroy(ctx->side[i]);
+  (void)hipStreamDestroy(ctx->stream);
+  (void)hipEventDestroy(ctx->ev_quot);
+  (void)hipEventDestroy(ctx->ev_scal);
+  delete ctx;
+}
+
+const char* zk_last_error(const zk_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+
+int zk_ctx_synchronize(zk_ctx* ctx) {
+  if (!ctx) return ZK_ERR_ARG;
+  ZK_GUARD(ctx, { ZK_HIP(hipStreamSynchronize(ctx->stream)); return ZK_OK; })
+}
+
+// ------------------------------------------------------------------ MSM ---
+template <class C, class ABI>
+static int msm_host(zk_ctx* ctx, const ABI* bases, size_t nb, const zk_fr* sc, size_t ns, uint32_t bits,
+                    ABI* out) {
+  if (!ctx || !out) return ZK_ERR_ARG;
+  if (nb != ns) return ZK_ERR_MSM_LEN;  // ark VariableBaseMSM::msm -> Err(min_len)
+  if (bits == 0 || bits > 256 || nb > 0x7fffffffull) return ZK_ERR_ARG;
+  ZK_GUARD(ctx, {
+    hipStream_t st = ctx->stream;
+    const int sw = bits <= 64 ? 1 : 4;
+    DevBuf raw, dev, scal;
+    raw.ensure(sizeof(ABI) * std::max<size_t>(nb, 1));
+    dev.ensure(sizeof(typename C::A) * std::max<size_t>(nb, 1));
+    scal.ensure(sizeof(uint64_t) * sw * std::max<size_t>(nb, 1));
+    if (nb) {
+      ZK_HIP(hipMemcpyAsync(raw.p, bases, sizeof(ABI) * nb, hipMemcpyHostToDevice, st));
+      if (sw == 4) {
+        ZK_HIP(hipMemcpyAsync(scal.p, sc, sizeof(zk_fr) * nb, hipMemcpyHostToDevice, st));
+      } else {
+        ZK_HIP(hipMemcpy2DAsync(scal.p, 8, sc, sizeof(zk_fr), 8, nb, hipMemcpyHostToDevice, st));
+      }
+      convert_bases<C>(raw.as<uint64_t>(), dev.as<typename C::A>(), nb, st);
+    }
+    MsmWork& w = ctx->msm[0];
+    msm_launch<C>(w, dev.as<typename C::A>(), scal.as<uint64_t>(), sw, (uint32_t)nb, sw == 1 ? 64 : 255, st);
+    msm_download<C>(w, st);
+    ZK_HIP(hipStreamSynchronize(st));
+    host_to_abi<C>(msm_finish<C>(w), reinterpret_cast<uint64_t*>(out));
+    return ZK_OK;
+  })
+}
+
+int zk_msm_g1(zk_ctx* ctx, const zk_g1_affine* bases, size_t nb, const zk_fr* sc, size_t ns, uint32_t bits,
+              zk_g1_affine* out) {
+  return msm_host<G1>(ctx, bases, nb, sc, ns, bits, out);
+}
+int zk_msm_g2(zk_ctx* ctx, const zk_g2_affine* bases, size_t nb, const zk_fr* sc, size_t ns, uint32_t bits,
+              zk_g2_affine* out) {
+  return msm_host<G2>(ctx, bases, nb, sc, ns, bits, out);
+}
+
+template <class C, class ABI>
+static int msm_upload(zk_ctx* ctx, const ABI* bases, size_t n, int group, zk_msm_bases** out) {
+  if (!ctx || !out) return ZK_ERR_ARG;
+  ZK_GUARD(ctx, {
+    std::unique_ptr<zk_msm_bases> b(new zk_msm_bases());
+    b->device = ctx->device;
+    b->group = group;
+    b->n = n;
+    b->bases.ensure(sizeof(typename C::A) * std::max<size_t>(n, 1));
+    DevBuf raw;
+    raw.ensure(sizeof(ABI) * std::max<size_t>(n, 1));
+    if (n) {
+      ZK_HIP(hipMemcpyAsync(raw.p, bases, sizeof(ABI) * n, hipMemcpyHostToDevice, ctx->stream));
+      convert_bases<C>(raw.as<uint64_t>(), b->bases.as<typename C::A>(), n, ctx->stream);
+    }
+    ZK_HIP(hipStreamSynchronize(ctx->stream));
+    *out = b.release();
+    return ZK_OK;
+  })
+}
+int zk_msm_g1_upload(zk_ctx* ctx, const zk_g1_affine* bases, size_t n, zk_msm_bases** out) {
+  return msm_upload<G1>(ctx, bases, n, 1, out);
+}
+int zk_msm_g2_upload(zk_ctx* ctx, const zk_g2_affine* bases, size_t n, zk_msm_bases** out) {
+  return msm_upload<G2>(ctx, bases, n, 2, out);
+}
+void zk_msm_bases_free(zk_msm_bases* b) {
+  if (!b) return;
+  (void)hipSetDevice(b->device);
+  delete b;
+}
+
+// Device scalars are canonical zk_fr (4 words).  64-bit mode reads the low
+// word of each (stride 4) through a compaction into the ctx scratch.
+__global__ void k_low_words(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = in[4 * i];
+}
+
+template <class C, class ABI>
+static int msm_dev(zk_ctx* ctx, const zk_msm_bases* b, const void* d_sc, size_t n, uint32_t bits, ABI* out,
+                   int group) {
+  if (!ctx || !b || !out || b->group != group) return ZK_ERR_ARG;
+  if (n != b->n) return ZK_ERR_MSM_LEN;
+  if (bits == 0 || bits > 256) return ZK_ERR_ARG;
+  ZK_GUARD(ctx, {
+    hipStream_t st = ctx->stream;
+    const uint64_t* sc = reinterpret_cast<const uint64_t*>(d_sc);
+    int sw = 4;
+    if (bits <= 64) {
+      ctx->tmp_scal.ensure(sizeof(uint64_t) * std::max<size_t>(n, 1));
+      if (n) {
+        k_low_words<<<ceil_div(n, 256), 256, 0, st>>>(sc, ctx->tmp_scal.as<uint64_t>(), n);
+        ZK_LAUNCH_CHECK();
+      }
+      sc = ctx->tmp_scal.as<uint64_t>();
+      sw = 1;
+    }
+    MsmWork& w = ctx->msm[0];
+    msm_launch<C>(w, b->bases.as<typename C::A>(), sc, sw, (uint32_t)n, sw == 1 ? 64 : 255, st);
+    msm_download<C>(w, st);
+    ZK_HIP(hipStreamSynchronize(st));
+    host_to_abi<C>(msm_finish<C>(w), reinterpret_cast<uint64_t*>(out));
+    return ZK_OK;
+  })
+}
+int zk_msm_g1_dev(zk_ctx* ctx, const zk_msm_bases* b, const void* d_sc, size_t n, uint32_t bits,
+                  zk_g1_affine* out) {
+  return msm_dev<G1>(ctx, b, d_sc, n, bits, out, 1);
+}
+int zk_msm_g2_dev(zk_ctx* ctx, const zk_msm_bases* b, const void* d_sc, size_t n, uint32_t bits,
+                  zk_g2_affine* out) {
+  return msm_dev<G2>(ctx, b, d_sc, n, bits, out, 2);
+}
+
+// ------------------------------------------------------------------ NTT ---
+static int ntt_device(zk_ctx* ctx, void* d_data, uint32_t log_n, int dir, const zk_fr* coset) {
+  hipStream_t st = ctx->stream;
+  const size_t n = (size_t)1 << log_n;
+  NttDomain& dom = ctx->domain(log_n);
+  ctx->tmp_fr.ensure(sizeof(Fr) * 2 * n);
+  Fr* a = ctx->tmp_fr.as<Fr>();
+  Fr* b = a + n;
+  auto to_dev = [](const host::Fr& h) { Fr d; std::memcpy(d.v, h.l, 32); return d; };
+  fr_to_mont(reinterpret_cast<const uint64_t*>(d_data), a, n, st);
+  const host::Fr one = host::fr_one();
+  const host::Fr ninv = host::fr_inv(host::fr_from_u64(n));
+  if (dir > 0) {
+    if (coset) {                                   // a_i *= g^i
+      fr_powers(b, to_dev(host::fr_to_mont(coset->l)), to_dev(one), n, st);
+      fr_scale_table(a, b, log_n, false, st);
+    }
+    ntt_dif(a, dom, false, st);                    // natural -> bit-reversed
+    fr_bitrev_copy(a, b, log_n, st);
+  } else {
+    ntt_dif(a, dom, true, st);
+    fr_bitrev_copy(a, b, log_n, st);
+    if (coset) {                                   // b_i *= n^-1 g^-i
+      host::Fr g = host::fr_to_mont(coset->l);
+      if (host::fr_is_zero(g)) return ZK_ERR_ARG;
+      fr_powers(a, to_dev(host::fr_inv(g)), to_dev(ninv), n, st);
+      fr_scale_table(b, a, log_n, false, st);
+    } else {
+      fr_scale_const(b, to_dev(ninv), n, st);
+    }
+  }
+  fr_from_mont(b, reinterpret_cast<uint64_t*>(d_data), n, st);
+  return ZK_OK;
+}
+
+int zk_ntt_fr_dev(zk_ctx* ctx, void* d_data, uint32_t log_n, int dir, const zk_fr* coset) {
+  if (!ctx || (dir != 1 && dir != -1)) return ZK_ERR_ARG;
+  if (log_n > 32) return ZK_ERR_DOMAIN;
+  ZK_GUARD(ctx, {
+    int rc = ntt_device(ctx, d_data, log_n, dir, coset);
+    ZK_HIP(hipStreamSynchronize(ctx->stream));
+    return rc;
+  })
+}
+
+int zk_ntt_fr(zk_ctx* ctx, zk_fr* data, uint32_t log_n, int dir, const zk_fr* coset) {
+  if (!ctx || !data || (dir != 1 && dir != -1)) return ZK_ERR_ARG;
+  if (log_n > 32) return ZK_ERR_DOMAIN;
+  ZK_GUARD(ctx, {
+    const size_t n = (size_t)1 << log_n;
+    DevBuf d;
+    d.ensure(sizeof(zk_fr) * n);
+    ZK_HIP(hipMemcpyAsync(d.p, data, sizeof(zk_fr) * n, hipMemcpyHostToDevice, ctx->stream));
+    int rc = ntt_device(ctx, d.p, log_n, dir, coset);
+    ZK_HIP(hipMemcpyAsync(data, d.p, sizeof(zk_fr) * n, hipMemcpyDeviceToHost, ctx->stream));
+    ZK_HIP(hipStreamSynchronize(ctx->stream));
+    return rc;
+  })
+}
+
+// ---------------------------------------------------------------- setup ---
+int zk_groth16_setup(zk_ctx* ctx, const zk_r1cs_csr* qap, const zk_setup_params* params, uint64_t num_public,
+                     zk_pk* pk, zk_vk* vk) {
+  if (!ctx || !qap || !params || !pk || !vk) return ZK_ERR_ARG;
+  ZK_GUARD(ctx, { return setup_impl(ctx, qap, params, num_public, 0, 1, pk, nullptr, vk); })
+}
+int zk_groth16_setup_dev(zk_ctx* ctx, const zk_r1cs_csr* qap, const zk_setup_params* params, uint64_t num_public,
+                         zk_pk_dev** out, zk_vk* vk) {
+  if (!ctx || !qap || !params || !out) return ZK_ERR_ARG;
+  ZK_GUARD(ctx, { return setup_impl(ctx, qap, params, num_public, 0, 1, nullptr, out, vk); })
+}
+int zk_groth16_setup_dev_shard(zk_ctx* ctx, const zk_r1cs_csr* qap, const zk_setup_params* params,
+                               uint64_t num_public, uint32_t shard, uint32_t nshards, zk_pk_dev** out) {
+  if (!ctx || !qap || !params || !out || nshards == 0 || shard >= nshards) return ZK_ERR_ARG;
+  ZK_GUARD(ctx, { return setup_impl(ctx, qap, params, num_public, shard, nshards, nullptr, out, nullptr); })
+}
+
+// ---------------------------------------------------------------- prove ---
+int zk_pk_upload(zk_ctx* ctx, const zk_pk* pk, const zk_r1cs_csr* qap, zk_pk_dev** out) {
+  if (!ctx || !pk || !qap || !out) return ZK_ERR_ARG;
+  ZK_GUARD(ctx, {
+    *out = pk_upload(ctx, pk, qap, 0, 1);
+    return ZK_OK;
+  })
+}
+int zk_pk_upload_shard(zk_ctx* ctx, const zk_pk* pk, const zk_r1cs_csr* qap, uint32_t shard, uint32_t nshards,
+                       zk_pk_dev** out) {
+  if (!ctx || !pk || !qap || !out || nshards == 0 || shard >= nshards) return ZK_ERR_ARG;
+  ZK_GUARD(ctx, {
+    *out = pk_upload(ctx, pk, qap, shard, nshards);
+    return ZK_OK;
+  })
+}
+void zk_pk_free(zk_pk_dev* pk) {
+  if (!pk) return;
+  (void)hipSetDevice(pk->device);
+  delete pk;
+}
+
+int zk_groth16_prove_dev(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, size_t zlen, size_t num_public,
+                         const zk_fr* r, const zk_fr* s, zk_proof* out) {
+  if (!ctx || !pk || !d_z || !r || !s || !out) return ZK_ERR_ARG;
+  ZK_GUARD(ctx, { return prove_impl(ctx, pk, d_z, zlen, num_public, r, s, out); })
+}
+
+int zk_groth16_prove(zk_ctx* ctx, const zk_pk_dev* pk, const zk_fr* z, size_t zlen, size_t num_public,
+                     const zk_fr* r, const zk_fr* s, zk_proof* out) {
+  if (!ctx || !pk || !z || !r || !s || !out) return ZK_ERR_ARG;
+  ZK_GUARD(ctx, {
+    ctx->z_canon.ensure(sizeof(zk_fr) * std::max<size_t>(zlen, 1));
+    if (zlen)
+      ZK_HIP(hipMemcpyAsync(ctx->z_canon.p, z, sizeof(zk_fr) * zlen, hipMemcpyHostToDevice, ctx->stream));
+    return prove_impl(ctx, pk, ctx->z_canon.p, zlen, num_public, r, s, out);
+  })
+}
+
+int zk_groth16_prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, size_t zlen, size_t num_public,
+                             const zk_fr* r, const zk_fr* s, zk_prove_partial* out) {
+  if (!ctx || !pk || !d_z || !r || !s || !out) return ZK_ERR_ARG;
+  ZK_GUARD(ctx, { return prove_partial_impl(ctx, pk, d_z, zlen, num_public, r, s, out); })
+}
+
+int zk_groth16_prove_combine(const zk_prove_partial* parts, size_t nparts, const zk_fr* r, const zk_fr* s,
+                             zk_proof* out) {
+  if (!parts || !nparts || !r || !s || !out) return ZK_ERR_ARG;
+  try {
+    return combine_impl(parts, nparts, r, s, out);
+  } catch (...) {
+    return ZK_ERR_DEVICE;
+  }
+}
+
+int zk_proof_serialize_compressed(const zk_proof* proof, uint8_t out[192]) {
+  if (!proof || !out) return ZK_ERR_ARG;
+  serialize_g1_compressed(proof->a, out);
+  serialize_g2_compressed(proof->b, out + 48);
+  serialize_g1_compressed(proof->c, out + 144);
+  return ZK_OK;
+}
+

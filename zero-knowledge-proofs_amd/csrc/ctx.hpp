@@ -1,0 +1,62 @@
+// ctx.hpp -- zk_ctx (one GPU: streams, cached NTT domains, MSM workspaces)
+// and zk_pk_dev (a proving key resident in HBM).
+#pragma once
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "msm.hpp"
+#include "ntt.hpp"
+
+namespace zk {
+
+constexpr int NUM_MSM = 5;  // pi_A (G1), pi_B (G2), B1 (G1), IC (G1), H (G1)
+enum MsmSlot { MSM_A = 0, MSM_B2 = 1, MSM_B1 = 2, MSM_IC = 3, MSM_H = 4 };
+
+// Device copy of the constraint matrices (the QAP in sparse form).
+struct CsrDev {
+  uint64_t nc = 0, V = 0;
+  DevBuf rp[3], col[3], val[3];
+  bool unit[3] = {false, false, false};
+};
+
+}  // namespace zk
+
+struct zk_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;                 // main stream
+  hipStream_t side[zk::NUM_MSM] = {};           // one stream per proof MSM
+  hipEvent_t ev_quot = nullptr, ev_scal = nullptr;
+  std::string err;
+  zk::MsmWork msm[zk::NUM_MSM];
+  std::map<uint32_t, std::unique_ptr<zk::NttDomain>> domains;
+  // prove scratch
+  zk::DevBuf z_canon, z_mont, qa, qb, qc, flags;
+  zk::DevBuf scal[zk::NUM_MSM];
+  zk::DevBuf tmp_bases, tmp_scal, tmp_fr;
+
+  zk::NttDomain& domain(uint32_t log_n);
+};
+
+struct zk_pk_dev {
+  int device = 0;
+  uint64_t V = 0, n = 0, nc = 0, num_public = 0;
+  uint32_t log_n = 0;
+  uint32_t shard = 0, nshards = 1;
+  zk::CsrDev csr;
+  // Compacted non-identity bases (device Montgomery affine) followed by the
+  // shard-0 extras, and the variable index feeding each base's scalar.
+  zk::DevBuf bases[zk::NUM_MSM];
+  zk::DevBuf idx[zk::NUM_MSM];      // u32 variable index per compacted base (H: coefficient index)
+  uint32_t count[zk::NUM_MSM] = {};  // compacted bases (without extras)
+  uint32_t extras[zk::NUM_MSM] = {}; // extra bases appended (shard 0 only)
+  uint32_t h_lo = 0, h_hi = 0;       // H coefficient range of this shard
+};
+
+struct zk_msm_bases {
+  int device = 0;
+  int group = 1;  // 1 = G1, 2 = G2
+  size_t n = 0;
+  zk::DevBuf bases;
+};

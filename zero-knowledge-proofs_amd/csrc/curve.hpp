@@ -1,0 +1,134 @@
+// curve.hpp -- BLS12-381 G1 (over Fq) / G2 (over Fq2) group law on device.
+//
+// The reference's group is ark-ec's short-Weierstrass Projective (Jacobian)
+// behind G1Projective / G2Projective (crates/groth16-core/src/lib.rs:16,
+// 275-300).  Group elements are unique, so any coordinate system yields the
+// same affine result; on device we use extended Jacobian "XYZZ" coordinates
+// (x = X/ZZ, y = Y/ZZZ, ZZ^3 = ZZZ^2) because the bucket-accumulate step is a
+// stream of XYZZ += affine additions (madd-2008-s: 8M + 2S, no inversion)
+// and the EFD formulas handle the degenerate cases with two branches.
+//
+// Device affine layout: Montgomery x then y, (0,0) = point at infinity
+// (0 != 4 so (0,0) is off-curve for both groups).
+#pragma once
+#include "ff.hpp"
+
+template <class F>
+struct Affine {
+  F x, y;
+};
+template <class F>
+struct XYZZ {
+  F X, Y, ZZ, ZZZ;
+};
+
+using G1A = Affine<Fq>;
+using G2A = Affine<Fq2>;
+using G1X = XYZZ<Fq>;
+using G2X = XYZZ<Fq2>;
+
+template <class F>
+ZK_DI bool aff_is_inf(const Affine<F>& a) {
+  return f_is_zero(a.x) && f_is_zero(a.y);
+}
+template <class F>
+ZK_DI void xyzz_set_inf(XYZZ<F>& p) {
+  f_set_zero(p.X); f_set_one(p.Y); f_set_zero(p.ZZ); f_set_zero(p.ZZZ);
+}
+template <class F>
+ZK_DI bool xyzz_is_inf(const XYZZ<F>& p) { return f_is_zero(p.ZZ); }
+
+template <class F>
+ZK_DI XYZZ<F> xyzz_from_aff(const Affine<F>& a) {
+  XYZZ<F> p;
+  if (aff_is_inf(a)) { xyzz_set_inf(p); return p; }
+  p.X = a.x; p.Y = a.y; f_set_one(p.ZZ); f_set_one(p.ZZZ);
+  return p;
+}
+
+// dbl-2008-s-1 (a = 0)
+template <class F>
+ZK_DI XYZZ<F> xyzz_dbl(const XYZZ<F>& p) {
+  F U = f_add(p.Y, p.Y);
+  F V = f_sqr(U);
+  F W = f_mul(U, V);
+  F S = f_mul(p.X, V);
+  F X2 = f_sqr(p.X);
+  F M = f_add(f_add(X2, X2), X2);
+  XYZZ<F> r;
+  r.X = f_sub(f_sqr(M), f_add(S, S));
+  r.Y = f_sub(f_mul(M, f_sub(S, r.X)), f_mul(W, p.Y));
+  r.ZZ = f_mul(V, p.ZZ);
+  r.ZZZ = f_mul(W, p.ZZZ);
+  return r;   // p at infinity (ZZ = 0) stays at infinity
+}
+
+// mdbl-2008-s-1: 2*a for affine a (not infinity)
+template <class F>
+ZK_DI XYZZ<F> aff_dbl(const Affine<F>& a) {
+  F U = f_add(a.y, a.y);
+  F V = f_sqr(U);
+  F W = f_mul(U, V);
+  F S = f_mul(a.x, V);
+  F X2 = f_sqr(a.x);
+  F M = f_add(f_add(X2, X2), X2);
+  XYZZ<F> r;
+  r.X = f_sub(f_sqr(M), f_add(S, S));
+  r.Y = f_sub(f_mul(M, f_sub(S, r.X)), f_mul(W, a.y));
+  r.ZZ = V;
+  r.ZZZ = W;
+  return r;
+}
+
+// madd-2008-s: p + a, a affine (a must not be infinity)
+template <class F>
+ZK_DI XYZZ<F> xyzz_madd(const XYZZ<F>& p, const Affine<F>& a) {
+  if (xyzz_is_inf(p)) return xyzz_from_aff(a);
+  F U2 = f_mul(a.x, p.ZZ);
+  F S2 = f_mul(a.y, p.ZZZ);
+  F P = f_sub(U2, p.X);
+  F R = f_sub(S2, p.Y);
+  if (f_is_zero(P)) {
+    if (f_is_zero(R)) return aff_dbl(a);
+    XYZZ<F> r; xyzz_set_inf(r); return r;
+  }
+  F PP = f_sqr(P);
+  F PPP = f_mul(P, PP);
+  F Q = f_mul(p.X, PP);
+  XYZZ<F> r;
+  r.X = f_sub(f_sub(f_sqr(R), PPP), f_add(Q, Q));
+  r.Y = f_sub(f_mul(R, f_sub(Q, r.X)), f_mul(p.Y, PPP));
+  r.ZZ = f_mul(p.ZZ, PP);
+  r.ZZZ = f_mul(p.ZZZ, PPP);
+  return r;
+}
+
+// add-2008-s: p + q
+template <class F>
+ZK_DI XYZZ<F> xyzz_add(const XYZZ<F>& p, const XYZZ<F>& q) {
+  if (xyzz_is_inf(p)) return q;
+  if (xyzz_is_inf(q)) return p;
+  F U1 = f_mul(p.X, q.ZZ);
+  F U2 = f_mul(q.X, p.ZZ);
+  F S1 = f_mul(p.Y, q.ZZZ);
+  F S2 = f_mul(q.Y, p.ZZZ);
+  F P = f_sub(U2, U1);
+  F R = f_sub(S2, S1);
+  if (f_is_zero(P)) {
+    if (f_is_zero(R)) return xyzz_dbl(p);
+    XYZZ<F> r; xyzz_set_inf(r); return r;
+  }
+  F PP = f_sqr(P);
+  F PPP = f_mul(P, PP);
+  F Q = f_mul(U1, PP);
+  XYZZ<F> r;
+  r.X = f_sub(f_sub(f_sqr(R), PPP), f_add(Q, Q));
+  r.Y = f_sub(f_mul(R, f_sub(Q, r.X)), f_mul(S1, PPP));
+  r.ZZ = f_mul(f_mul(p.ZZ, q.ZZ), PP);
+  r.ZZZ = f_mul(f_mul(p.ZZZ, q.ZZZ), PPP);
+  return r;
+}
+
+template <class F>
+ZK_DI Affine<F> aff_neg(const Affine<F>& a) { return {a.x, f_neg(a.y)}; }
+

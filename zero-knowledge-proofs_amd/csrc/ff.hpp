@@ -1,0 +1,250 @@
+// ff.hpp -- device prime-field arithmetic for gfx950 (CDNA4).
+//
+// Mirrors ark-ff 0.4.2's Fp<MontBackend<_, N64>, N64> (the Fr / Fq behind
+// groth16-field's `F`, crates/groth16-field/src/lib.rs:14-17): Montgomery form
+// with R = 2^(64*N64), little-endian limbs.  On device the same bytes are
+// handled as 2*N64 32-bit limbs so that every limb product is one
+// v_mad_u64_u32 (32x32+64 -> 64) -- the widest integer multiply CDNA4 has.
+// No MFMA: this is carry-chained modular arithmetic, not a contraction.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "constants.hpp"
+
+#define ZK_DI __device__ __forceinline__
+
+// 16-byte vector global loads / stores of whole field elements / points
+template <class T>
+ZK_DI T ld_vec(const T* p) {
+  static_assert(sizeof(T) % 16 == 0, "16-byte multiple");
+  T r;
+  const uint4* s = reinterpret_cast<const uint4*>(p);
+  uint4* d = reinterpret_cast<uint4*>(&r);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 16); i++) d[i] = s[i];
+  return r;
+}
+template <class T>
+ZK_DI void st_vec(T* p, const T& v) {
+  static_assert(sizeof(T) % 16 == 0, "16-byte multiple");
+  const uint4* s = reinterpret_cast<const uint4*>(&v);
+  uint4* d = reinterpret_cast<uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 16); i++) d[i] = s[i];
+}
+
+template <class P>
+struct Fp {
+  uint32_t v[P::N];
+};
+
+using Fq = Fp<FqParams>;
+using Fr = Fp<FrParams>;
+
+template <class P>
+ZK_DI Fp<P> fp_zero() {
+  Fp<P> r;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) r.v[i] = 0;
+  return r;
+}
+template <class P>
+ZK_DI Fp<P> fp_one() {
+  Fp<P> r;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) r.v[i] = P::ONE[i];
+  return r;
+}
+template <class P>
+ZK_DI Fp<P> fp_from_const(const uint32_t (&c)[P::N]) {
+  Fp<P> r;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) r.v[i] = c[i];
+  return r;
+}
+template <class P>
+ZK_DI bool fp_is_zero(const Fp<P>& a) {
+  uint32_t x = a.v[0];
+#pragma unroll
+  for (int i = 1; i < P::N; i++) x |= a.v[i];
+  return x == 0;
+}
+template <class P>
+ZK_DI bool fp_eq(const Fp<P>& a, const Fp<P>& b) {
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) x |= a.v[i] ^ b.v[i];
+  return x == 0;
+}
+
+// r = a - m if a >= m else a   (a < 2m)
+template <class P>
+ZK_DI Fp<P> fp_reduce_once(const Fp<P>& a) {
+  Fp<P> s;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) s.v[i] = __builtin_subc(a.v[i], P::MOD[i], br, &br);
+  Fp<P> r;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) r.v[i] = br ? a.v[i] : s.v[i];
+  return r;
+}
+
+template <class P>
+ZK_DI Fp<P> fp_add(const Fp<P>& a, const Fp<P>& b) {
+  Fp<P> r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) r.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+  return fp_reduce_once(r);   // a + b < 2m < 2^(32N): no carry out
+}
+template <class P>
+ZK_DI Fp<P> fp_dbl(const Fp<P>& a) { return fp_add(a, a); }
+
+template <class P>
+ZK_DI Fp<P> fp_sub(const Fp<P>& a, const Fp<P>& b) {
+  Fp<P> r;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) r.v[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
+  uint32_t mask = 0u - br, c = 0;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) r.v[i] = __builtin_addc(r.v[i], P::MOD[i] & mask, c, &c);
+  return r;
+}
+template <class P>
+ZK_DI Fp<P> fp_neg(const Fp<P>& a) { return fp_sub(fp_zero<P>(), a); }
+
+// Montgomery product a*b/R mod m, CIOS with the "no-carry" shortcut (valid
+// because the top 32-bit word of both moduli is < 2^31 - 1).  Each limb
+// product-accumulate is one v_mad_u64_u32.
+template <class P>
+ZK_DI Fp<P> fp_mul(const Fp<P>& a, const Fp<P>& b) {
+  constexpr int N = P::N;
+  uint32_t t[N], bb[N];
+#pragma unroll
+  for (int j = 0; j < N; j++) { t[j] = 0; bb[j] = b.v[j]; }
+  // Outer loop deliberately NOT unrolled: one ~4N-instruction body per limb
+  // of b keeps a 381-bit multiply at ~100 instructions of code, so EC
+  // formulas (10-30 multiplies) fit the instruction cache.  b is rotated so
+  // every register index stays static.
+#pragma unroll 1
+  for (int i = 0; i < N; i++) {
+    const uint32_t bi = bb[0];
+#pragma unroll
+    for (int j = 0; j < N - 1; j++) bb[j] = bb[j + 1];
+    uint64_t A = (uint64_t)a.v[0] * bi + t[0];
+    t[0] = (uint32_t)A;
+    const uint32_t m = t[0] * P::INV;
+    uint64_t C = (uint64_t)m * P::MOD[0] + t[0];
+#pragma unroll
+    for (int j = 1; j < N; j++) {
+      A = (uint64_t)a.v[j] * bi + t[j] + (A >> 32);
+      t[j] = (uint32_t)A;
+      C = (uint64_t)m * P::MOD[j] + t[j] + (C >> 32);
+      t[j - 1] = (uint32_t)C;
+    }
+    t[N - 1] = (uint32_t)(C >> 32) + (uint32_t)(A >> 32);
+  }
+  Fp<P> r;
+#pragma unroll
+  for (int j = 0; j < N; j++) r.v[j] = t[j];
+  return fp_reduce_once(r);
+}
+template <class P>
+ZK_DI Fp<P> fp_sqr(const Fp<P>& a) { return fp_mul(a, a); }
+
+template <class P>
+ZK_DI Fp<P> fp_to_mont(const Fp<P>& canon) { return fp_mul(canon, fp_from_const<P>(P::R2)); }
+template <class P>
+ZK_DI Fp<P> fp_from_mont(const Fp<P>& a) {
+  Fp<P> one;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) one.v[i] = i == 0 ? 1u : 0u;
+  return fp_mul(a, one);
+}
+// a^(m-2): Fermat inversion (0 -> 0)
+template <class P>
+ZK_DI Fp<P> fp_inv(const Fp<P>& a) {
+  uint32_t e[P::N];
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) e[i] = __builtin_subc(P::MOD[i], i == 0 ? 2u : 0u, br, &br);
+  Fp<P> acc = fp_one<P>();
+  for (int i = P::N - 1; i >= 0; i--) {
+    for (int k = 31; k >= 0; k--) {
+      acc = fp_sqr(acc);
+      if ((e[i] >> k) & 1) acc = fp_mul(acc, a);
+    }
+  }
+  return acc;
+}
+
+ZK_DI Fq fq_mul(const Fq& a, const Fq& b) { return fp_mul(a, b); }
+
+ZK_DI Fq fq_inv(const Fq& a) {
+  uint32_t e[12];
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) e[i] = __builtin_subc(FqParams::MOD[i], i == 0 ? 2u : 0u, br, &br);
+  Fq acc = fp_one<FqParams>();
+#pragma unroll
+  for (int i = 11; i >= 0; i--) {
+    for (int k = 31; k >= 0; k--) {
+      acc = fq_mul(acc, acc);
+      if ((e[i] >> k) & 1) acc = fq_mul(acc, a);
+    }
+  }
+  return acc;
+}
+
+// ---------------------------------------------------------------- Fq2 -----
+// Fq2 = Fq[u]/(u^2 + 1)  (ark-bls12-381 Fq2Config NONRESIDUE = -1)
+struct Fq2 {
+  Fq c0, c1;
+};
+ZK_DI Fq2 fq2_zero() { return {fp_zero<FqParams>(), fp_zero<FqParams>()}; }
+ZK_DI Fq2 fq2_one() { return {fp_one<FqParams>(), fp_zero<FqParams>()}; }
+ZK_DI bool fq2_is_zero(const Fq2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+ZK_DI Fq2 fq2_add(const Fq2& a, const Fq2& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
+ZK_DI Fq2 fq2_sub(const Fq2& a, const Fq2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+ZK_DI Fq2 fq2_neg(const Fq2& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
+ZK_DI Fq2 fq2_mul(const Fq2& a, const Fq2& b) {
+  Fq t0 = fq_mul(a.c0, b.c0);
+  Fq t1 = fq_mul(a.c1, b.c1);
+  Fq m = fq_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  return {fp_sub(t0, t1), fp_sub(fp_sub(m, t0), t1)};
+}
+ZK_DI Fq2 fq2_sqr(const Fq2& a) {
+  // (c0 + c1 u)^2 = (c0+c1)(c0-c1) + 2 c0 c1 u
+  Fq m = fq_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  Fq t = fq_mul(a.c0, a.c1);
+  return {m, fp_add(t, t)};
+}
+ZK_DI Fq2 fq2_inv(const Fq2& a) {
+  Fq n = fp_add(fq_mul(a.c0, a.c0), fq_mul(a.c1, a.c1));
+  n = fq_inv(n);
+  return {fq_mul(a.c0, n), fp_neg(fq_mul(a.c1, n))};
+}
+
+// Generic field-op shims so curve code is written once for Fq and Fq2.
+ZK_DI Fq f_add(const Fq& a, const Fq& b) { return fp_add(a, b); }
+ZK_DI Fq f_sub(const Fq& a, const Fq& b) { return fp_sub(a, b); }
+ZK_DI Fq f_mul(const Fq& a, const Fq& b) { return fq_mul(a, b); }
+ZK_DI Fq f_sqr(const Fq& a) { return fq_mul(a, a); }
+ZK_DI Fq f_neg(const Fq& a) { return fp_neg(a); }
+ZK_DI bool f_is_zero(const Fq& a) { return fp_is_zero(a); }
+ZK_DI Fq f_inv(const Fq& a) { return fq_inv(a); }
+ZK_DI void f_set_zero(Fq& a) { a = fp_zero<FqParams>(); }
+ZK_DI void f_set_one(Fq& a) { a = fp_one<FqParams>(); }
+
+ZK_DI Fq2 f_add(const Fq2& a, const Fq2& b) { return fq2_add(a, b); }
+ZK_DI Fq2 f_sub(const Fq2& a, const Fq2& b) { return fq2_sub(a, b); }
+ZK_DI Fq2 f_mul(const Fq2& a, const Fq2& b) { return fq2_mul(a, b); }
+ZK_DI Fq2 f_sqr(const Fq2& a) { return fq2_sqr(a); }
+ZK_DI Fq2 f_neg(const Fq2& a) { return fq2_neg(a); }
+ZK_DI bool f_is_zero(const Fq2& a) { return fq2_is_zero(a); }
+ZK_DI Fq2 f_inv(const Fq2& a) { return fq2_inv(a); }
+ZK_DI void f_set_zero(Fq2& a) { a = fq2_zero(); }
+ZK_DI void f_set_one(Fq2& a) { a = fq2_one(); }

@@ -1,0 +1,51 @@
+// ntt.hpp -- radix-2 NTT over BLS12-381 Fr on gfx950.
+//
+// Replaces ark-poly 0.4.2 Radix2EvaluationDomain::{fft, ifft} and the coset
+// variants as used by QAP::from_r1cs (crates/groth16-qap/src/lib.rs:101,
+// 167-169) and by DensePolynomial mul / divide_by_vanishing_poly inside
+// compute_quotient_polynomial (qap:260-263).  Same domain generator as ark:
+// omega_n = (7^((r-1)/2^32))^(2^(32 - log n)).
+//
+// Layout: Fr elements are 32 B (8 x u32 Montgomery limbs), contiguous.
+// A pass loads a tile of 2^ns rows x C consecutive columns into LDS
+// (<= 2048 elements = 64 KiB), runs ns radix-2 stages with workgroup
+// barriers, and writes it back: log n stages cost ceil(log n / ~9) HBM
+// round trips instead of log n.  DIF passes take natural order to
+// bit-reversed order, DIT passes the reverse, so the quotient pipeline
+// (iNTT -> coset NTT -> divide -> coset iNTT) never needs a standalone
+// permutation except once, fused into its final gather.
+#pragma once
+#include "common.hpp"
+#include "ff.hpp"
+
+namespace zk {
+
+// Per-domain constant tables, built on device once and cached by the ctx.
+struct NttDomain {
+  uint32_t log_n = 0;
+  DevBuf tw;      // omega^k, k < n/2
+  DevBuf itw;     // omega^-k, k < n/2
+  DevBuf gpow;    // n^-1 * g^i, i < n   (coset shift g = 7)
+  DevBuf gipow;   // n^-1 * g^-i, i < n
+  DevBuf zinv;    // (g^n - 1)^-1: 1/Z on the coset g<w>
+};
+
+void ntt_domain_init(NttDomain& d, uint32_t log_n, hipStream_t st);
+
+// In-place passes over n Montgomery Fr.
+void ntt_dif(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st);
+void ntt_dit(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st);
+
+// Elementwise helpers
+void fr_to_mont(const uint64_t* d_canon, Fr* d_out, size_t n, hipStream_t st);
+void fr_from_mont(const Fr* d_in, uint64_t* d_canon, size_t n, hipStream_t st);
+// data[p] *= tab[bitrev(p)] (bitrev over log_n bits)  or  tab[p] when !bitrev
+void fr_scale_table(Fr* d_data, const Fr* d_tab, uint32_t log_n, bool bitrev, hipStream_t st);
+// out[i] = in[bitrev(i)] (out-of-place)
+void fr_bitrev_copy(const Fr* d_in, Fr* d_out, uint32_t log_n, hipStream_t st);
+// data[i] *= c (Montgomery constant)
+void fr_scale_const(Fr* d_data, const Fr& c_host, size_t n, hipStream_t st);
+// out[i] = base^i * scale (Montgomery), i < n
+void fr_powers(Fr* d_out, const Fr& base, const Fr& scale, size_t n, hipStream_t st);
+
+}  // namespace zk

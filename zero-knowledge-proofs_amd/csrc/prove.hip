@@ -1,0 +1,418 @@
+// prove.hip -- Groth16 prove() orchestration on one GPU.
+//
+// Restates Prover::prove (crates/groth16-core/src/lib.rs:139-272) with the
+// reference's arithmetic, quirks included:
+//   w_i = lo64(z_i)                                         core:156-161
+//   pi_A = alpha_1 + sum w_i a_g1[i] + r delta_1            core:164-179
+//   pi_B = beta_2  + sum w_i b_g2[i] + s delta_2            core:182-197
+//   H    = (A B - C) / (x^n - 1), h_i = lo64(H_i)           core:200-208, qap:225-271
+//   H_1  = sum h_i h_g1[i]                                  core:211-221
+//   B_1  = beta_1  + sum w_i b_g1[i]                        core:246-255
+//   pi_C = sum_{i>l} w_i ic_g1[i-l-1] + H_1 + s pi_A + r B_1  core:224-265
+// Every sum is one device MSM with 64-bit scalars: the full-width terms
+// r*delta_1 and s*delta_2 are split as sum_k r_k (2^(64k) delta) over four
+// precomputed bases (appended at pk upload), identity bases are compacted
+// away at upload (they contribute nothing), and only s*pi_A + r*B_1 -- which
+// depend on this proof's own MSM outputs -- are formed on the host.
+#include <algorithm>
+#include <cstring>
+
+#include "ctx.hpp"
+
+namespace zk {
+
+// ------------------------------------------------------------------ CSR ---
+__global__ void __launch_bounds__(256) k_u64_to_fr_mont(const uint64_t* __restrict__ in, Fr* __restrict__ out,
+                                                        size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  st_vec(&out[i], fp_to_mont(ld_vec(reinterpret_cast<const Fr*>(in) + i)));
+}
+
+void csr_upload(CsrDev& d, const zk_r1cs_csr* q, hipStream_t st) {
+  d.nc = q->num_constraints;
+  d.V = q->num_variables;
+  const uint64_t* rps[3] = {q->a_rowptr, q->b_rowptr, q->c_rowptr};
+  const uint32_t* cols[3] = {q->a_col, q->b_col, q->c_col};
+  const zk_fr* vals[3] = {q->a_val, q->b_val, q->c_val};
+  for (int m = 0; m < 3; m++) {
+    const uint64_t nnz = d.nc ? rps[m][d.nc] : 0;
+    d.rp[m].ensure(sizeof(uint64_t) * (d.nc + 1));
+    ZK_HIP(hipMemcpyAsync(d.rp[m].p, rps[m], sizeof(uint64_t) * (d.nc + 1), hipMemcpyHostToDevice, st));
+    d.col[m].ensure(sizeof(uint32_t) * std::max<uint64_t>(nnz, 1));
+    if (nnz) ZK_HIP(hipMemcpyAsync(d.col[m].p, cols[m], sizeof(uint32_t) * nnz, hipMemcpyHostToDevice, st));
+    d.unit[m] = vals[m] == nullptr;
+    if (!d.unit[m] && nnz) {
+      DevBuf tmp;
+      tmp.ensure(sizeof(zk_fr) * nnz);
+      ZK_HIP(hipMemcpyAsync(tmp.p, vals[m], sizeof(zk_fr) * nnz, hipMemcpyHostToDevice, st));
+      d.val[m].ensure(sizeof(Fr) * nnz);
+      k_u64_to_fr_mont<<<ceil_div(nnz, 256), 256, 0, st>>>(tmp.as<uint64_t>(), d.val[m].as<Fr>(), nnz);
+      ZK_LAUNCH_CHECK();
+      ZK_HIP(hipStreamSynchronize(st));  // tmp dies here
+    }
+  }
+}
+
+struct CsrArgs {
+  const uint64_t* rp[3];
+  const uint32_t* col[3];
+  const Fr* val[3];
+};
+
+__device__ __forceinline__ Fr row_dot(const uint64_t* __restrict__ rp, const uint32_t* __restrict__ col,
+                                      const Fr* __restrict__ val, uint64_t row, const Fr* __restrict__ zc,
+                                      uint64_t V) {
+  Fr acc = fp_zero<FrParams>();
+  const uint64_t e = rp[row + 1];
+  for (uint64_t k = rp[row]; k < e; k++) {
+    const uint32_t c = col[k];
+    if (c >= V) continue;                   // qap:122-124
+    Fr zv = fp_to_mont(ld_vec(&zc[c]));
+    if (val) zv = fp_mul(zv, ld_vec(&val[k]));
+    acc = fp_add(acc, zv);
+  }
+  return acc;
+}
+
+// (Az)_j, (Bz)_j, (Cz)_j for every domain row (rows >= nc are zero padding,
+// qap:155-164) plus the witness checks:
+//   flags bit 0: row vrow unsatisfied      -> InvalidWitness (core:121-128: the
+//                reference checks A(w)B(w) = C(w) at w = omega, i.e. row 1,
+//                or row 0 when n == 1)
+//   flags bit 1: some row unsatisfied      -> PolynomialDivisionFailed (qap:266)
+//   flags bit 2: z_0 != 1                  -> InvalidWitness (core:89-93)
+__global__ void __launch_bounds__(256) k_csr_eval(CsrArgs m, const Fr* __restrict__ zc, uint64_t nc, uint64_t V,
+                                                  uint64_t n, uint64_t vrow, Fr* __restrict__ qa,
+                                                  Fr* __restrict__ qb, Fr* __restrict__ qc,
+                                                  uint32_t* __restrict__ flags) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j == 0) {
+    Fr z0 = ld_vec(&zc[0]);
+    bool one = z0.v[0] == 1;
+#pragma unroll
+    for (int i = 1; i < 8; i++) one = one && z0.v[i] == 0;
+    if (!one) atomicOr(flags, 4u);
+  }
+  if (j >= n) return;
+  Fr a = fp_zero<FrParams>(), b = a, c = a;
+  if (j < nc) {
+    a = row_dot(m.rp[0], m.col[0], m.val[0], j, zc, V);
+    b = row_dot(m.rp[1], m.col[1], m.val[1], j, zc, V);
+    c = row_dot(m.rp[2], m.col[2], m.val[2], j, zc, V);
+    if (!fp_eq(fp_mul(a, b), c)) atomicOr(flags, j == vrow ? 3u : 2u);
+  }
+  st_vec(&qa[j], a);
+  st_vec(&qb[j], b);
+  st_vec(&qc[j], c);
+}
+
+__global__ void __launch_bounds__(256) k_quot_pointwise(Fr* __restrict__ qa, const Fr* __restrict__ qb,
+                                                        const Fr* __restrict__ qc, const Fr* __restrict__ zinv,
+                                                        size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Fr t = fp_sub(fp_mul(ld_vec(&qa[i]), ld_vec(&qb[i])), ld_vec(&qc[i]));
+  st_vec(&qa[i], fp_mul(t, ld_vec(zinv)));
+}
+
+__device__ __forceinline__ uint32_t brev(uint32_t x, uint32_t log_n) {
+  return log_n ? (__builtin_bitreverse32(x) >> (32 - log_n)) : 0;
+}
+
+// H_i = n^-1 g^-i * (bit-reversed iNTT output)[i], then lo64 (core:203-208)
+__global__ void __launch_bounds__(256) k_h_final(const Fr* __restrict__ hb, const Fr* __restrict__ gipow,
+                                                 uint32_t log_n, uint64_t* __restrict__ hlo) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >> log_n) return;
+  Fr h = fp_from_mont(fp_mul(ld_vec(&hb[brev((uint32_t)i, log_n)]), ld_vec(&gipow[i])));
+  hlo[i] = (uint64_t)h.v[0] | ((uint64_t)h.v[1] << 32);
+}
+
+__global__ void __launch_bounds__(256) k_gather_lo64(const uint64_t* __restrict__ src, int stride_words,
+                                                     const uint32_t* __restrict__ idx, uint32_t count,
+                                                     uint64_t* __restrict__ out) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  out[k] = src[(size_t)idx[k] * stride_words];
+}
+
+// ------------------------------------------------------------- pk upload ---
+static uint64_t shard_lo(uint64_t len, uint32_t k, uint32_t ns) { return len * k / ns; }
+
+// host XYZZ from canonical ABI affine words
+static host::X<host::Fq> g1_from_abi(const zk_g1_affine& a) {
+  if (a.infinity) return host::inf<host::Fq>();
+  host::X<host::Fq> p;
+  std::memcpy(p.X_.l, a.x, 48);
+  std::memcpy(p.Y.l, a.y, 48);
+  p.X_ = host::to_mont(p.X_);
+  p.Y = host::to_mont(p.Y);
+  p.ZZ = host::one();
+  p.ZZZ = host::one();
+  return p;
+}
+static host::X<host::Fq2> g2_from_abi(const zk_g2_affine& a) {
+  if (a.infinity) return host::inf<host::Fq2>();
+  host::X<host::Fq2> p;
+  std::memcpy(p.X_.c0.l, a.x, 48);
+  std::memcpy(p.X_.c1.l, a.x + 6, 48);
+  std::memcpy(p.Y.c0.l, a.y, 48);
+  std::memcpy(p.Y.c1.l, a.y + 6, 48);
+  p.X_ = {host::to_mont(p.X_.c0), host::to_mont(p.X_.c1)};
+  p.Y = {host::to_mont(p.Y.c0), host::to_mont(p.Y.c1)};
+  p.ZZ = host::f_one<host::Fq2>();
+  p.ZZZ = host::f_one<host::Fq2>();
+  return p;
+}
+
+// [P, 2^64 P, 2^128 P, 2^192 P] in ABI form
+template <class C, class ABI>
+static void pow64_chain(const host::X<typename C::HF>& P, ABI* out) {
+  host::X<typename C::HF> q = P;
+  for (int k = 0; k < 4; k++) {
+    host_to_abi<C>(q, reinterpret_cast<uint64_t*>(&out[k]));
+    for (int d = 0; d < 64; d++) q = host::dbl(q);
+  }
+}
+
+// Upload one base vector range [lo, hi): compact non-identity entries, append extras.
+template <class C, class ABI>
+static void upload_vector(zk_pk_dev& pk, int slot, const ABI* v, uint64_t lo, uint64_t hi, uint64_t idx_offset,
+                          const std::vector<ABI>& extras, hipStream_t st) {
+  std::vector<uint32_t> idx;
+  idx.reserve(hi - lo);
+  for (uint64_t i = lo; i < hi; i++)
+    if (!v[i].infinity) idx.push_back((uint32_t)(i - lo));
+  const uint32_t cnt = (uint32_t)idx.size();
+  const uint32_t nex = (uint32_t)extras.size();
+  pk.count[slot] = cnt;
+  pk.extras[slot] = nex;
+  pk.bases[slot].ensure(sizeof(typename C::A) * std::max<uint64_t>(cnt + nex, 1));
+  pk.idx[slot].ensure(sizeof(uint32_t) * std::max<uint32_t>(cnt, 1));
+  DevBuf raw, didx;
+  raw.ensure(sizeof(ABI) * std::max<uint64_t>(hi - lo, 1));
+  didx.ensure(sizeof(uint32_t) * std::max<uint32_t>(cnt, 1));
+  if (hi > lo) ZK_HIP(hipMemcpyAsync(raw.p, v + lo, sizeof(ABI) * (hi - lo), hipMemcpyHostToDevice, st));
+  if (cnt) ZK_HIP(hipMemcpyAsync(didx.p, idx.data(), sizeof(uint32_t) * cnt, hipMemcpyHostToDevice, st));
+  convert_bases_gather<C>(raw.as<uint64_t>(), didx.as<uint32_t>(), pk.bases[slot].as<typename C::A>(), cnt, st);
+  // scalar index = variable / coefficient index
+  std::vector<uint32_t> gidx(cnt);
+  for (uint32_t k = 0; k < cnt; k++) gidx[k] = (uint32_t)(idx[k] + lo + idx_offset);
+  if (cnt) ZK_HIP(hipMemcpyAsync(pk.idx[slot].p, gidx.data(), sizeof(uint32_t) * cnt, hipMemcpyHostToDevice, st));
+  if (nex) {
+    DevBuf ex;
+    ex.ensure(sizeof(ABI) * nex);
+    ZK_HIP(hipMemcpyAsync(ex.p, extras.data(), sizeof(ABI) * nex, hipMemcpyHostToDevice, st));
+    convert_bases<C>(ex.as<uint64_t>(), pk.bases[slot].as<typename C::A>() + cnt, nex, st);
+    ZK_HIP(hipStreamSynchronize(st));
+  }
+  ZK_HIP(hipStreamSynchronize(st));  // host vectors / staging die here
+}
+
+zk_pk_dev* pk_upload(zk_ctx* ctx, const zk_pk* pk, const zk_r1cs_csr* q, uint32_t shard, uint32_t nshards) {
+  hipStream_t st = ctx->stream;
+  std::unique_ptr<zk_pk_dev> d(new zk_pk_dev());
+  d->device = ctx->device;
+  d->V = q->num_variables;
+  d->nc = q->num_constraints;
+  d->n = 1;
+  while (d->n < d->nc) d->n <<= 1;
+  d->log_n = (uint32_t)__builtin_ctzll(d->n);
+  d->num_public = pk->num_public;
+  d->shard = shard;
+  d->nshards = nshards;
+  csr_upload(d->csr, q, st);
+  const bool first = shard == 0;
+  // extras: pi_A gets alpha_1 (scalar 1) and 2^(64k) delta_1 (scalar r_k);
+  // pi_B gets beta_2 and 2^(64k) delta_2 (s_k); B_1 gets beta_1.
+  std::vector<zk_g1_affine> exA, exB1, none1;
+  std::vector<zk_g2_affine> exB2;
+  if (first) {
+    exA.resize(5);
+    exA[0] = pk->alpha_g1;
+    pow64_chain<G1>(g1_from_abi(pk->delta_g1), &exA[1]);
+    exB2.resize(5);
+    exB2[0] = pk->beta_g2;
+    pow64_chain<G2>(g2_from_abi(pk->delta_g2), &exB2[1]);
+    exB1.push_back(pk->beta_g1);
+  }
+  const uint64_t V = d->V;
+  {
+    const uint64_t L = std::min<uint64_t>(pk->a_len, V);  // core:171 i < a_g1.len()
+    uint64_t lo = shard_lo(L, shard, nshards), hi = shard_lo(L, shard + 1, nshards);
+    upload_vector<G1>(*d, MSM_A, pk->a_g1, lo, hi, 0, exA, st);
+  }
+  {
+    const uint64_t L = std::min<uint64_t>(pk->b2_len, V);  // core:189
+    uint64_t lo = shard_lo(L, shard, nshards), hi = shard_lo(L, shard + 1, nshards);
+    upload_vector<G2>(*d, MSM_B2, pk->b_g2, lo, hi, 0, exB2, st);
+  }
+  {
+    const uint64_t L = std::min<uint64_t>(pk->b_len, V);  // core:250
+    uint64_t lo = shard_lo(L, shard, nshards), hi = shard_lo(L, shard + 1, nshards);
+    upload_vector<G1>(*d, MSM_B1, pk->b_g1, lo, hi, 0, exB1, st);
+  }
+  {
+    // ic_g1[k] pairs with variable k + num_public + 1 (core:227-231)
+    uint64_t L = std::min<uint64_t>(pk->ic_len, V > pk->num_public + 1 ? V - pk->num_public - 1 : 0);
+    uint64_t lo = shard_lo(L, shard, nshards), hi = shard_lo(L, shard + 1, nshards);
+    upload_vector<G1>(*d, MSM_IC, pk->ic_g1, lo, hi, pk->num_public + 1, none1, st);
+  }
+  {
+    // h_g1[i] pairs with H coefficient i (zip, core:211-215); H has n coefficients
+    uint64_t L = std::min<uint64_t>(pk->h_len, d->n);
+    uint64_t lo = shard_lo(L, shard, nshards), hi = shard_lo(L, shard + 1, nshards);
+    d->h_lo = (uint32_t)lo;
+    d->h_hi = (uint32_t)hi;
+    upload_vector<G1>(*d, MSM_H, pk->h_g1, lo, hi, 0, none1, st);
+  }
+  // the a/b vectors may be shorter than V (core:171 `i < pk.a_g1.len()`): indices stay < V.
+  return d.release();
+}
+
+// ---------------------------------------------------------------- prove ---
+// Partial accumulators of one shard (host XYZZ, Montgomery).
+struct Partial {
+  host::X<host::Fq> A, B1, IC, H;
+  host::X<host::Fq2> B2;
+  int32_t status;
+};
+static_assert(sizeof(Partial) <= ZK_PARTIAL_BYTES, "partial size");
+
+static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipStream_t st) {
+  const uint64_t n = pk->n;
+  NttDomain& dom = ctx->domain(pk->log_n);
+  ctx->qa.ensure(sizeof(Fr) * n);
+  ctx->qb.ensure(sizeof(Fr) * n);
+  ctx->qc.ensure(sizeof(Fr) * n);
+  CsrArgs m;
+  for (int k = 0; k < 3; k++) {
+    m.rp[k] = pk->csr.rp[k].as<uint64_t>();
+    m.col[k] = pk->csr.col[k].as<uint32_t>();
+    m.val[k] = pk->csr.unit[k] ? nullptr : pk->csr.val[k].as<Fr>();
+  }
+  const uint64_t vrow = n > 1 ? 1 : 0;
+  k_csr_eval<<<ceil_div(n, 256), 256, 0, st>>>(m, reinterpret_cast<const Fr*>(d_z), pk->nc, pk->V, n, vrow,
+                                                ctx->qa.as<Fr>(), ctx->qb.as<Fr>(), ctx->qc.as<Fr>(),
+                                                ctx->flags.as<uint32_t>());
+  ZK_LAUNCH_CHECK();
+  Fr* v[3] = {ctx->qa.as<Fr>(), ctx->qb.as<Fr>(), ctx->qc.as<Fr>()};
+  for (int k = 0; k < 3; k++) {
+    ntt_dif(v[k], dom, /*inverse twiddles*/ true, st);                   // coefficients * n, bit-reversed
+    fr_scale_table(v[k], dom.gpow.as<Fr>(), pk->log_n, true, st);        // * n^-1 g^i
+    ntt_dit(v[k], dom, false, st);                                       // evaluations on g<w>, natural
+  }
+  k_quot_pointwise<<<ceil_div(n, 256), 256, 0, st>>>(v[0], v[1], v[2], dom.zinv.as<Fr>(), n);
+  ZK_LAUNCH_CHECK();
+  ntt_dif(v[0], dom, true, st);
+  ctx->scal[MSM_H].ensure(sizeof(uint64_t) * n);
+  ctx->tmp_scal.ensure(sizeof(uint64_t) * n);
+  k_h_final<<<ceil_div(n, 256), 256, 0, st>>>(v[0], dom.gipow.as<Fr>(), pk->log_n, ctx->tmp_scal.as<uint64_t>());
+  ZK_LAUNCH_CHECK();
+}
+
+static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, const zk_fr* r,
+                             const zk_fr* s) {
+  hipStream_t st = ctx->stream;
+  ctx->flags.ensure(16);
+  ZK_HIP(hipMemsetAsync(ctx->flags.p, 0, 16, st));
+  quotient(ctx, pk, d_z, st);  // (Az, Bz, Cz) -> lo64(H) in tmp_scal
+  // scalars: lo64 of the assignment (or of H) gathered per compacted base, + extras
+  for (int slot = 0; slot < NUM_MSM; slot++) {
+    const uint32_t cnt = pk->count[slot], nex = pk->extras[slot];
+    ctx->scal[slot].ensure(sizeof(uint64_t) * std::max<uint32_t>(cnt + nex, 1));
+    if (cnt) {
+      const uint64_t* src = slot == MSM_H ? ctx->tmp_scal.as<uint64_t>() : d_z;
+      const int stride = slot == MSM_H ? 1 : 4;
+      k_gather_lo64<<<ceil_div(cnt, 256), 256, 0, st>>>(src, stride, pk->idx[slot].as<uint32_t>(), cnt,
+                                                         ctx->scal[slot].as<uint64_t>());
+      ZK_LAUNCH_CHECK();
+    }
+    if (nex) {
+      uint64_t ex[5] = {1, 0, 0, 0, 0};
+      const zk_fr* full = slot == MSM_A ? r : slot == MSM_B2 ? s : nullptr;
+      if (full) for (int k = 0; k < 4; k++) ex[1 + k] = full->l[k];
+      ZK_HIP(hipMemcpyAsync(ctx->scal[slot].as<uint64_t>() + cnt, ex, sizeof(uint64_t) * nex,
+                            hipMemcpyHostToDevice, st));
+      ZK_HIP(hipStreamSynchronize(st));  // ex is a stack buffer
+    }
+  }
+  for (int slot = 0; slot < NUM_MSM; slot++) {
+    const uint32_t n = pk->count[slot] + pk->extras[slot];
+    if (slot == MSM_B2)
+      msm_launch<G2>(ctx->msm[slot], pk->bases[slot].as<G2A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64, st);
+    else
+      msm_launch<G1>(ctx->msm[slot], pk->bases[slot].as<G1A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64, st);
+  }
+  uint32_t flags = 0;
+  ZK_HIP(hipMemcpyAsync(&flags, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
+  for (int slot = 0; slot < NUM_MSM; slot++) {
+    if (slot == MSM_B2) msm_download<G2>(ctx->msm[slot], st);
+    else msm_download<G1>(ctx->msm[slot], st);
+  }
+  ZK_HIP(hipStreamSynchronize(st));
+  Partial p{};
+  p.status = ZK_OK;
+  if (flags & 5u) p.status = ZK_ERR_INVALID_WITNESS;
+  else if (flags & 2u) p.status = ZK_ERR_QAP_DIVISION;
+  if (p.status != ZK_OK) return p;
+  p.A = msm_finish<G1>(ctx->msm[MSM_A]);
+  p.B2 = msm_finish<G2>(ctx->msm[MSM_B2]);
+  p.B1 = msm_finish<G1>(ctx->msm[MSM_B1]);
+  p.IC = msm_finish<G1>(ctx->msm[MSM_IC]);
+  p.H = msm_finish<G1>(ctx->msm[MSM_H]);
+  return p;
+}
+
+static int combine(const Partial* parts, size_t k, const zk_fr* r, const zk_fr* s, zk_proof* out) {
+  for (size_t i = 0; i < k; i++)
+    if (parts[i].status != ZK_OK) return parts[i].status;
+  auto A = host::inf<host::Fq>(), B1 = A, IC = A, H = A;
+  auto B2 = host::inf<host::Fq2>();
+  for (size_t i = 0; i < k; i++) {
+    A = host::addp(A, parts[i].A);
+    B1 = host::addp(B1, parts[i].B1);
+    IC = host::addp(IC, parts[i].IC);
+    H = host::addp(H, parts[i].H);
+    B2 = host::addp(B2, parts[i].B2);
+  }
+  // pi_C = IC + H_1 + s pi_A + r B_1 (core:224-265; identity terms add nothing)
+  auto C = host::addp(host::addp(IC, H),
+                      host::addp(host::mul_scalar(A, s->l), host::mul_scalar(B1, r->l)));
+  host_to_abi<G1>(A, reinterpret_cast<uint64_t*>(&out->a));
+  host_to_abi<G2>(B2, reinterpret_cast<uint64_t*>(&out->b));
+  host_to_abi<G1>(C, reinterpret_cast<uint64_t*>(&out->c));
+  return ZK_OK;
+}
+
+int prove_impl(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, size_t zlen, size_t num_public,
+               const zk_fr* r, const zk_fr* s, zk_proof* out) {
+  // Witness::new (core:81-99) and the length check of validate (core:113-118)
+  if (num_public >= zlen) return ZK_ERR_INVALID_WITNESS;
+  if (zlen != pk->V) return ZK_ERR_INVALID_WITNESS;
+  if (pk->nshards != 1) return ZK_ERR_ARG;
+  Partial p = prove_partial(ctx, pk, reinterpret_cast<const uint64_t*>(d_z), r, s);
+  return combine(&p, 1, r, s, out);
+}
+
+int prove_partial_impl(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, size_t zlen, size_t num_public,
+                       const zk_fr* r, const zk_fr* s, zk_prove_partial* out) {
+  std::memset(out, 0, sizeof *out);
+  Partial p{};
+  if (num_public >= zlen || zlen != pk->V) {
+    p.status = ZK_ERR_INVALID_WITNESS;
+  } else {
+    p = prove_partial(ctx, pk, reinterpret_cast<const uint64_t*>(d_z), r, s);
+  }
+  std::memcpy(out->bytes, &p, sizeof p);
+  return p.status;
+}
+
+int combine_impl(const zk_prove_partial* parts, size_t k, const zk_fr* r, const zk_fr* s, zk_proof* out) {
+  std::vector<Partial> ps(k);
+  for (size_t i = 0; i < k; i++) std::memcpy(&ps[i], parts[i].bytes, sizeof(Partial));
+  return combine(ps.data(), k, r, s, out);
+}
+
+}  // namespace zk

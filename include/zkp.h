@@ -100,6 +100,15 @@ zk_ctx *zk_ctx_create(int device);
 void zk_ctx_destroy(zk_ctx *ctx);
 const char *zk_last_error(const zk_ctx *ctx);
 int zk_ctx_synchronize(zk_ctx *ctx);
+/* Live kernel timing: HIP events recorded on the launching stream around
+ * each kernel phase (msm_sort, msm_accum_g1, msm_accum_g2, msm_reduce, ntt,
+ * quotient_eval, quotient_misc).  No reference counterpart (measurement). */
+int zk_ctx_profile(zk_ctx *ctx, int enable);
+/* names: '\0'-separated phase names; per phase: total ms, launches, work
+ * units (scalar-point pairs for msm_*, elements for ntt/quotient). */
+int zk_ctx_profile_read(zk_ctx *ctx, char *names, size_t names_cap, double *ms,
+                        uint64_t *launches, uint64_t *units, size_t max_phases,
+                        size_t *nphases);
 
 /* ---------------------------------------------------------------- MSM --- */
 /* Sum_i scalars[i] * bases[i], normalised to affine.  Replaces

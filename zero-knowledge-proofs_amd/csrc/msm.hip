@@ -21,34 +21,34 @@ MsmPlan msm_make_plan(uint32_t n, int bits, int sw, int force_c) {
     if (nwin > MSM_MAXWIN) continue;
     int top = bits - c * (nwin - 1);
     double nbuck = (double)(nwin - 1) * (1u << (c - 1)) + (double)(1u << top);
-    // accumulate: one mixed add per (point, window); reduce: ~3 full adds per bucket
-    double cost = (double)n * nwin + 4.0 * nbuck;
+    // accumulate: one mixed add per (point, window); reduce: ~2.5 full adds per bucket
+    double cost = (double)n * nwin + 3.5 * nbuck;
     if (cost < best) { best = cost; best_c = c; }
   }
   if (force_c) best_c = force_c;
   p.c = best_c;
   p.nwin = (bits + p.c - 1) / p.c;
-  p.L = 8;
-  p.K = 16;
-  uint32_t G = 0, T = 0;
-  int maxT = 1;
+  p.K = 32;
+  uint32_t G = 0, rc = 0, q = 0;
   for (int w = 0; w < p.nwin; w++) {
-    int width = (w == p.nwin - 1) ? bits - p.c * w : p.c;
-    p.nb[w] = (w == p.nwin - 1) ? (1u << width) : (1u << (p.c - 1));
+    const int width = (w == p.nwin - 1) ? bits - p.c * w : p.c;
+    const int k = (w == p.nwin - 1) ? width : p.c - 1;   // nb = 2^k
+    p.nb[w] = 1u << k;
+    p.kr[w] = (uint8_t)(k / 2);
+    p.kc[w] = (uint8_t)(k - k / 2);
     p.boff[w] = G;
-    p.segoff[w] = T;
+    p.rcoff[w] = rc;
+    p.qoff[w] = q;
     G += p.nb[w];
-    uint32_t t = ceil_div(p.nb[w], p.L);
-    T += t;
-    maxT = std::max<int>(maxT, (int)t);
+    rc += (1u << p.kr[w]) + (1u << p.kc[w]);
+    q += p.kr[w] + p.kc[w] + 1;
   }
   p.boff[p.nwin] = G;
-  p.segoff[p.nwin] = T;
+  p.rcoff[p.nwin] = rc;
+  p.qoff[p.nwin] = q;
   p.G = G;
-  p.T = T;
-  int qb = 0;
-  while ((1 << qb) < maxT) qb++;
-  p.Q = 1 + qb;
+  p.nrc = rc;
+  p.nq = q;
   return p;
 }
 
@@ -111,30 +111,72 @@ __global__ void __launch_bounds__(256) k_msm_digits(const uint64_t* __restrict__
   }
 }
 
-// Exclusive scan of G counts by one 1024-thread workgroup.
-__global__ void __launch_bounds__(1024) k_msm_scan(const uint32_t* __restrict__ counts, uint32_t G,
-                                                   uint32_t* __restrict__ off, uint32_t* __restrict__ cur) {
-  __shared__ uint32_t part[1024];
+// --------------------------------------------------------------- scan ---
+// 3-phase exclusive scan of G bucket counts: per-block sums, one scan of
+// the block sums, per-block scan with its base.  Writes off[0..G] and a
+// copy in cursor[] for the scatter.
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sh, uint32_t& total) {
   const uint32_t t = threadIdx.x;
-  const uint32_t per = (G + 1023) / 1024;
-  const uint32_t b = min(t * per, G), e = min(b + per, G);
+  sh[t] = v;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {
+    uint32_t x = t >= d ? sh[t - d] : 0;
+    __syncthreads();
+    sh[t] += x;
+    __syncthreads();
+  }
+  total = sh[255];
+  uint32_t r = sh[t] - v;
+  __syncthreads();
+  return r;
+}
+__global__ void __launch_bounds__(256) k_scan_local(const uint32_t* __restrict__ counts, uint32_t G,
+                                                    uint32_t* __restrict__ part) {
+  __shared__ uint32_t sh[256];
+  const uint32_t base = blockIdx.x * MSM_SCAN_BLOCK + threadIdx.x * 4;
   uint32_t s = 0;
-  for (uint32_t i = b; i < e; i++) s += counts[i];
-  part[t] = s;
+#pragma unroll
+  for (int k = 0; k < 4; k++) s += base + k < G ? counts[base + k] : 0;
+  uint32_t tot;
+  block_excl_scan256(s, sh, tot);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+__global__ void __launch_bounds__(1024) k_scan_part(uint32_t* __restrict__ part, uint32_t nblk) {
+  __shared__ uint32_t sh[1024];
+  const uint32_t t = threadIdx.x;
+  const uint32_t v = t < nblk ? part[t] : 0;
+  sh[t] = v;
   __syncthreads();
   for (uint32_t d = 1; d < 1024; d <<= 1) {
-    uint32_t v = t >= d ? part[t - d] : 0;
+    uint32_t x = t >= d ? sh[t - d] : 0;
     __syncthreads();
-    part[t] += v;
+    sh[t] += x;
     __syncthreads();
   }
-  uint32_t base = t ? part[t - 1] : 0;
-  for (uint32_t i = b; i < e; i++) {
-    off[i] = base;
-    cur[i] = base;
-    base += counts[i];
+  if (t < nblk) part[t] = sh[t] - v;
+}
+__global__ void __launch_bounds__(256) k_scan_down(const uint32_t* __restrict__ counts, uint32_t G,
+                                                   const uint32_t* __restrict__ part, uint32_t* __restrict__ off,
+                                                   uint32_t* __restrict__ cur) {
+  __shared__ uint32_t sh[256];
+  const uint32_t base = blockIdx.x * MSM_SCAN_BLOCK + threadIdx.x * 4;
+  uint32_t c[4], s = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    c[k] = base + k < G ? counts[base + k] : 0;
+    s += c[k];
   }
-  if (t == 1023) off[G] = part[1023];
+  uint32_t tot;
+  uint32_t x = block_excl_scan256(s, sh, tot) + part[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (base + k < G) {
+      off[base + k] = x;
+      cur[base + k] = x;
+    }
+    if (base + k == G - 1) off[G] = x + c[k];
+    x += c[k];
+  }
 }
 
 // --------------------------------------------------------- accumulate ---
@@ -147,9 +189,9 @@ __device__ __forceinline__ typename C::A load_point(const typename C::A* __restr
 
 // Thread t owns sorted entries [tK, tK+K).  One mixed add per entry (uniform
 // across the wave); at a bucket change the finished run is flushed:
-//   complete bucket        -> buckets[g]
-//   run begun by an earlier thread (head) -> partials[2t]
-//   run continued by a later thread (tail) -> partials[2t+1]
+//   complete bucket                        -> buckets[g]
+//   run begun by an earlier thread (head)   -> partials[2t]
+//   run continued by a later thread (tail)  -> partials[2t+1]
 template <class C>
 __global__ void __launch_bounds__(128) k_msm_accum(const typename C::A* __restrict__ bases,
                                                    const uint32_t* __restrict__ ent,
@@ -203,54 +245,81 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
   st_vec(&buckets[g], acc);
 }
 
-// Per (window, segment of L buckets): running sum from the top bucket down.
-//   S_j = sum of the segment's buckets, W_j = sum_m (m+1) B_{jL+m}.
-template <class C>
-__global__ void __launch_bounds__(128) k_msm_reduce1(MsmPlan p, const uint32_t* __restrict__ off,
-                                                     const typename C::X* __restrict__ buckets,
-                                                     typename C::X* __restrict__ segS,
-                                                     typename C::X* __restrict__ segW) {
-  using X = typename C::X;
-  const uint32_t sid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (sid >= p.T) return;
-  int w = 0;
-  while (sid >= p.segoff[w + 1]) w++;
-  const uint32_t j = sid - p.segoff[w];
-  const uint32_t lo = p.boff[w] + j * p.L;
-  const uint32_t hi = min(lo + (uint32_t)p.L, p.boff[w] + p.nb[w]);
-  X run, sum;
-  xyzz_set_inf(run);
-  xyzz_set_inf(sum);
-  for (uint32_t g = hi; g-- > lo;) {
-    if (off[g + 1] != off[g]) run = xyzz_add(run, ld_vec(&buckets[g]));
-    sum = xyzz_add(sum, run);
-  }
-  st_vec(&segS[sid], run);
-  st_vec(&segW[sid], sum);
-}
-
-// One workgroup per (window, quantity q): q = 0 -> sum_j W_j;
-// q = 1 + b -> U_b = sum over segments j with bit b set of S_j.
-template <class C, int NT>
-__global__ void __launch_bounds__(NT) k_msm_reduce2(MsmPlan p, const typename C::X* __restrict__ segS,
-                                                    const typename C::X* __restrict__ segW,
-                                                    typename C::X* __restrict__ res) {
-  using X = typename C::X;
-  __shared__ X sh[NT];
-  const int w = blockIdx.x / p.Q, q = blockIdx.x % p.Q;
-  const uint32_t T = p.segoff[w + 1] - p.segoff[w];
-  const X* src = (q == 0 ? segW : segS) + p.segoff[w];
-  X acc;
-  xyzz_set_inf(acc);
-  for (uint32_t j = threadIdx.x; j < T; j += NT)
-    if (q == 0 || ((j >> (q - 1)) & 1)) acc = xyzz_add(acc, ld_vec(&src[j]));
-  sh[threadIdx.x] = acc;
+// ------------------------------------------------------------- reduce ---
+// Workgroup-wide plain sum of one XYZZ per thread (tree over the first
+// `len` threads' values; the result lands in sh[0]).
+template <class X>
+__device__ __forceinline__ void tree_sum(X* sh, X v, uint32_t len) {
+  const uint32_t t = threadIdx.x;
+  sh[t] = v;
   __syncthreads();
-  for (int d = NT / 2; d > 0; d >>= 1) {
-    if ((int)threadIdx.x < d) sh[threadIdx.x] = xyzz_add(sh[threadIdx.x], sh[threadIdx.x + d]);
+  uint32_t p2 = 1;
+  while (p2 < len) p2 <<= 1;
+  for (uint32_t d = p2 >> 1; d > 0; d >>= 1) {
+    if (t < d && t + d < len) sh[t] = xyzz_add(sh[t], sh[t + d]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) st_vec(&res[blockIdx.x], sh[0]);
+}
+
+// One workgroup per row (C_hi, 2^kc contiguous buckets) or column
+// (D_lo, 2^kr buckets at stride 2^kc) of every window.  <= 256 buckets each.
+template <class C>
+__global__ void __launch_bounds__(256) k_msm_rowcol(MsmPlan p, const uint32_t* __restrict__ off,
+                                                    const typename C::X* __restrict__ buckets,
+                                                    typename C::X* __restrict__ rc) {
+  using X = typename C::X;
+  __shared__ X sh[256];
+  const uint32_t b = blockIdx.x;
+  int w = 0;
+  while (b >= p.rcoff[w + 1]) w++;
+  const uint32_t i = b - p.rcoff[w];
+  const uint32_t rows = 1u << p.kr[w], cols = 1u << p.kc[w];
+  uint32_t len, g0, stride;
+  if (i < rows) {
+    len = cols; g0 = p.boff[w] + i * cols; stride = 1;
+  } else {
+    len = rows; g0 = p.boff[w] + (i - rows); stride = cols;
+  }
+  X v;
+  xyzz_set_inf(v);
+  const uint32_t t = threadIdx.x;
+  if (t < len) {
+    const uint32_t g = g0 + t * stride;
+    if (off[g + 1] != off[g]) v = ld_vec(&buckets[g]);
+  }
+  tree_sum(sh, v, len);
+  if (t == 0) st_vec(&rc[b], sh[0]);
+}
+
+// One workgroup per quantity: U^C_b (rows with bit b), U^D_b (columns with
+// bit b), P (all columns) of every window.
+template <class C>
+__global__ void __launch_bounds__(256) k_msm_quant(MsmPlan p, const typename C::X* __restrict__ rc,
+                                                   typename C::X* __restrict__ res) {
+  using X = typename C::X;
+  __shared__ X sh[256];
+  const uint32_t b = blockIdx.x;
+  int w = 0;
+  while (b >= p.qoff[w + 1]) w++;
+  const uint32_t q = b - p.qoff[w];
+  const uint32_t kr = p.kr[w], kc = p.kc[w];
+  const uint32_t rows = 1u << kr, cols = 1u << kc;
+  const uint32_t t = threadIdx.x;
+  uint32_t len;
+  bool take;
+  const X* src;
+  if (q < kr) {               // U^C_q
+    len = rows; src = rc + p.rcoff[w]; take = (t >> q) & 1;
+  } else if (q < kr + kc) {   // U^D_{q-kr}
+    len = cols; src = rc + p.rcoff[w] + rows; take = (t >> (q - kr)) & 1;
+  } else {                    // P
+    len = cols; src = rc + p.rcoff[w] + rows; take = true;
+  }
+  X v;
+  xyzz_set_inf(v);
+  if (t < len && take) v = ld_vec(&src[t]);
+  tree_sum(sh, v, len);
+  if (t == 0) st_vec(&res[b], sh[0]);
 }
 
 // ------------------------------------------------------------ driver -----
@@ -260,20 +329,26 @@ void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scal
   using X = typename C::X;
   MsmPlan& p = w.plan;
   p = msm_make_plan(n, bits, sw);
+  if (p.G > (uint32_t)MSM_SCAN_BLOCK * 1024) throw Error(ZK_ERR_ARG, "msm: too many buckets");
   const size_t M = (size_t)n * p.nwin;
+  if (M >= 0x80000000ull) throw Error(ZK_ERR_ARG, "msm: too many (point, window) entries");
+  const uint32_t nblk = ceil_div(p.G, MSM_SCAN_BLOCK);
   w.counts.ensure(sizeof(uint32_t) * (p.G + 1));
   w.off.ensure(sizeof(uint32_t) * (p.G + 1));
   w.cursor.ensure(sizeof(uint32_t) * (p.G + 1));
+  w.scan_part.ensure(sizeof(uint32_t) * nblk);
   w.ent.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
   w.key.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
   w.buckets.ensure(sizeof(X) * p.G);
   const size_t nthr_max = (M + p.K - 1) / p.K + 1;
   w.partials.ensure(sizeof(X) * 2 * nthr_max);
-  w.segS.ensure(sizeof(X) * p.T);
-  w.segW.ensure(sizeof(X) * p.T);
-  w.res.ensure(sizeof(X) * p.nwin * p.Q);
+  w.rc.ensure(sizeof(X) * p.nrc);
+  w.res.ensure(sizeof(X) * p.nq);
 
+  Prof* pf = w.prof;
+  const bool g2 = sizeof(typename C::A) == sizeof(G2A);
   ZK_HIP(hipMemsetAsync(w.counts.p, 0, sizeof(uint32_t) * (p.G + 1), st));
+  int ph = pf ? pf->begin(st, "msm_sort", n) : -1;   // digits + scan + scatter
   if (n) {
     const uint32_t nb = ceil_div(n, 256);
     if (sw == 1)
@@ -282,7 +357,12 @@ void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scal
       k_msm_digits<4, false><<<nb, 256, 0, st>>>(d_scalars, p, w.counts.as<uint32_t>(), nullptr, nullptr, nullptr);
     ZK_LAUNCH_CHECK();
   }
-  k_msm_scan<<<1, 1024, 0, st>>>(w.counts.as<uint32_t>(), p.G, w.off.as<uint32_t>(), w.cursor.as<uint32_t>());
+  k_scan_local<<<nblk, 256, 0, st>>>(w.counts.as<uint32_t>(), p.G, w.scan_part.as<uint32_t>());
+  ZK_LAUNCH_CHECK();
+  k_scan_part<<<1, 1024, 0, st>>>(w.scan_part.as<uint32_t>(), nblk);
+  ZK_LAUNCH_CHECK();
+  k_scan_down<<<nblk, 256, 0, st>>>(w.counts.as<uint32_t>(), p.G, w.scan_part.as<uint32_t>(),
+                                    w.off.as<uint32_t>(), w.cursor.as<uint32_t>());
   ZK_LAUNCH_CHECK();
   if (n) {
     const uint32_t nb = ceil_div(n, 256);
@@ -294,62 +374,66 @@ void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scal
                                                 w.ent.as<uint32_t>(), w.key.as<uint32_t>());
     ZK_LAUNCH_CHECK();
   }
+  if (pf) pf->end(st, ph);
   // The number of non-zero digits M' <= M is only known on device: launch for
-  // M threads' worth of chunks; chunks beyond off[G] exit immediately.  To
-  // avoid a host sync we bound M' by M.
-  const uint32_t Mtot = (uint32_t)M;
-  if (Mtot) {
-    const uint32_t nthr = ceil_div(Mtot, p.K);
+  // M entries' worth of chunks; chunks beyond off[G] exit at once (no host sync).
+  if (M) {
+    const uint32_t nthr = ceil_div(M, p.K);
+    ph = pf ? pf->begin(st, g2 ? "msm_accum_g2" : "msm_accum_g1", n) : -1;
     k_msm_accum<C><<<ceil_div(nthr, 128), 128, 0, st>>>(d_bases, w.ent.as<uint32_t>(), w.key.as<uint32_t>(),
-                                                           w.off.as<uint32_t>(), p.G, p.K, w.buckets.as<X>(),
-                                                           w.partials.as<X>());
+                                                         w.off.as<uint32_t>(), p.G, p.K, w.buckets.as<X>(),
+                                                         w.partials.as<X>());
     ZK_LAUNCH_CHECK();
+    if (pf) pf->end(st, ph);
   }
+  ph = pf ? pf->begin(st, "msm_reduce", p.G) : -1;   // fixup + row/col + quantities
   k_msm_fixup<C><<<ceil_div(p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), p.G, p.K, w.buckets.as<X>(),
                                                       w.partials.as<X>());
   ZK_LAUNCH_CHECK();
-  k_msm_reduce1<C><<<ceil_div(p.T, 128), 128, 0, st>>>(p, w.off.as<uint32_t>(), w.buckets.as<X>(),
-                                                        w.segS.as<X>(), w.segW.as<X>());
+  k_msm_rowcol<C><<<p.nrc, 256, 0, st>>>(p, w.off.as<uint32_t>(), w.buckets.as<X>(), w.rc.as<X>());
   ZK_LAUNCH_CHECK();
-  k_msm_reduce2<C, 128><<<p.nwin * p.Q, 128, 0, st>>>(p, w.segS.as<X>(), w.segW.as<X>(), w.res.as<X>());
+  k_msm_quant<C><<<p.nq, 256, 0, st>>>(p, w.rc.as<X>(), w.res.as<X>());
   ZK_LAUNCH_CHECK();
+  if (pf) pf->end(st, ph);
 }
-
 
 template <class C>
 void msm_download(MsmWork& w, hipStream_t st) {
   using X = typename C::X;
-  const size_t bytes = sizeof(X) * w.plan.nwin * w.plan.Q;
-  w.host_res.resize(bytes);
-  ZK_HIP(hipMemcpyAsync(w.host_res.data(), w.res.p, bytes, hipMemcpyDeviceToHost, st));
+  const size_t bytes = sizeof(X) * w.plan.nq;
+  w.host_res.ensure(bytes);
+  ZK_HIP(hipMemcpyAsync(w.host_res.p, w.res.p, bytes, hipMemcpyDeviceToHost, st));
 }
 
 // Device XYZZ (32-bit limbs) and host XYZZ (64-bit limbs) share their bytes.
+// Every quantity is a point times a power of two:
+//   U^C_b : 2^(c w + kc + b),  U^D_b : 2^(c w + b),  P : 2^(c w)
+// so one Horner pass over exponents from the top combines everything.
 template <class C>
 host::X<typename C::HF> msm_finish(const MsmWork& w) {
   using HF = typename C::HF;
   using HX = host::X<HF>;
   static_assert(sizeof(HX) == sizeof(typename C::X), "layout");
   const MsmPlan& p = w.plan;
-  const HX* r = reinterpret_cast<const HX*>(w.host_res.data());
-  // Every partial is a point times a power of two:
-  //   window w, q = 0     : 2^(c w)              * W-sum
-  //   window w, q = 1 + b : 2^(c w + log2 L + b) * U_b
-  // One Horner pass over exponents from the top.
-  int lgL = 0;
-  while ((1 << lgL) < p.L) lgL++;
+  const HX* r = w.host_res.as<const HX>();
   int maxe = 0;
-  for (int w = 0; w < p.nwin; w++) maxe = std::max(maxe, p.c * w + lgL + p.Q - 2);
+  for (int win = 0; win < p.nwin; win++)
+    maxe = std::max(maxe, p.c * win + std::max<int>(p.kc[win] + p.kr[win] - 1, p.kc[win]));
   std::vector<std::vector<const HX*>> at(maxe + 1);
-  for (int w = 0; w < p.nwin; w++)
-    for (int q = 0; q < p.Q; q++) {
-      int e = q == 0 ? p.c * w : p.c * w + lgL + (q - 1);
-      at[e].push_back(&r[w * p.Q + q]);
+  for (int win = 0; win < p.nwin; win++) {
+    const int kr = p.kr[win], kc = p.kc[win];
+    for (int q = 0; q < kr + kc + 1; q++) {
+      int e = q < kr ? p.c * win + kc + q : q < kr + kc ? p.c * win + (q - kr) : p.c * win;
+      at[e].push_back(&r[p.qoff[win] + q]);
     }
+  }
   HX acc = host::inf<HF>();
+  auto host_form = [](const HX& d) {   // device Montgomery radix -> host radix, per coordinate
+    return HX{host::to_host(d.X_), host::to_host(d.Y), host::to_host(d.ZZ), host::to_host(d.ZZZ)};
+  };
   for (int e = maxe; e >= 0; e--) {
     acc = host::dbl(acc);
-    for (const HX* t : at[e]) acc = host::addp(acc, *t);
+    for (const HX* t : at[e]) acc = host::addp(acc, host_form(*t));
   }
   return acc;
 }

@@ -6,23 +6,28 @@
 // element sum_i k_i P_i, so the algorithm may differ from ark's while the
 // normalised affine output is bit-identical.
 //
-// Pipeline per MSM (all on one HIP stream, workspace reused):
-//   1 count    signed c-bit window digits, bucket histogram (global atomics)
-//   2 scan     exclusive scan of bucket counts -> bucket offsets
+// Pipeline per MSM (one HIP stream; workspace reused across calls):
+//   1 digits   signed c-bit window digits -> bucket histogram (global atomics)
+//   2 scan     3-phase parallel exclusive scan -> bucket offsets
 //   3 scatter  (point index | sign) entries grouped by bucket (counting sort)
-//   4 accum    fixed K entries per thread, XYZZ += affine, run-length flush:
-//              load-balanced whatever the digit distribution
-//   5 fixup    buckets split across threads: sum the <= 2 partials per thread
-//   6 reduce1  per (window, L-bucket segment) running sums -> S_j, W_j
-//   7 reduce2  per window: sum_j W_j and U_b = sum_{j: bit b of j} S_j
-//   host tail  sum_w 2^(c w) (sum W + L sum_b 2^b U_b): one Horner pass over
-//              the ~nwin*(Q) partials (latency-bound; see host_ec.hpp)
+//   4 accum    fixed K entries per thread, XYZZ += affine with run-length
+//              flush: load-balanced whatever the digit distribution
+//   5 fixup    buckets split across threads: sum the per-thread partials
+//   6 rowcol   window w's nb = 2^(kr+kc) buckets seen as a 2^kr x 2^kc grid,
+//              bucket m = hi*2^kc + lo has weight m+1 = hi*2^kc + lo + 1, so
+//              sum_m (m+1) B_m = 2^kc sum_hi hi C_hi + sum_lo (lo+1) D_lo with
+//              C = row sums, D = column sums: 2 nb plain adds, tree depth 8
+//   7 quant    U^C_b = sum_{hi: bit b} C_hi, U^D_b = sum_{lo: bit b} D_lo,
+//              P = sum_lo D_lo: one masked tree (depth <= 8) per quantity
+//   host tail  sum_w 2^(c w) (2^kc sum_b 2^b U^C_b + sum_b 2^b U^D_b + P):
+//              one Horner pass over ~16 nwin partials (latency-bound; see
+//              host_ec.hpp for why this tail runs on the host)
 #pragma once
+#include <vector>
+
 #include "common.hpp"
 #include "curve.hpp"
 #include "host_ec.hpp"
-
-#include <vector>
 
 namespace zk {
 
@@ -42,25 +47,29 @@ struct G2 {
 };
 
 constexpr int MSM_MAXWIN = 64;
+constexpr int MSM_SCAN_BLOCK = 1024;  // elements per scan block (256 threads x 4)
 
 struct MsmPlan {
-  int c, nwin, bits, sw;           // window bits, #windows, scalar bits, u64 words/scalar
-  int L, K, Q;                     // reduce segment, accumulate chunk, reduce2 quantities
-  uint32_t n;                      // points
-  uint32_t G;                      // total buckets
-  uint32_t T;                      // total reduce segments
-  uint32_t nb[MSM_MAXWIN];         // buckets in window w (digits 1..nb)
-  uint32_t boff[MSM_MAXWIN + 1];   // first global bucket id of window w
-  uint32_t segoff[MSM_MAXWIN + 1]; // first reduce segment of window w
+  int c, nwin, bits, sw;            // window bits, #windows, scalar bits, u64 words/scalar
+  int K;                            // accumulate chunk (entries per thread)
+  uint32_t n;                       // points
+  uint32_t G;                       // total buckets
+  uint32_t nrc, nq;                 // total row/col sums, total quantities
+  uint32_t nb[MSM_MAXWIN];          // buckets in window w (digits 1..nb), a power of two
+  uint32_t boff[MSM_MAXWIN + 1];    // first global bucket id of window w
+  uint8_t kr[MSM_MAXWIN], kc[MSM_MAXWIN];   // nb = 2^(kr + kc): rows x columns
+  uint32_t rcoff[MSM_MAXWIN + 1];   // first row/col sum of window w (rows, then columns)
+  uint32_t qoff[MSM_MAXWIN + 1];    // first quantity of window w (U^C, U^D, P)
 };
 
 MsmPlan msm_make_plan(uint32_t n, int bits, int sw, int force_c = 0);
 
 // Device workspace of one in-flight MSM.
 struct MsmWork {
-  DevBuf counts, off, cursor, ent, key, buckets, partials, segS, segW, res;
-  std::vector<uint8_t> host_res;
+  DevBuf counts, off, cursor, scan_part, ent, key, buckets, partials, rc, res;
+  PinnedBuf host_res;
   MsmPlan plan{};
+  Prof* prof = nullptr;  // optional live kernel timing
 };
 
 // Launch the device part of an MSM over n Montgomery-affine device bases and

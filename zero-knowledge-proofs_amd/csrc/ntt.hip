@@ -83,9 +83,10 @@ static uint32_t pass_stages(uint32_t s_lo, uint32_t remaining) {
   return std::min(cap, remaining);
 }
 
-void ntt_dif(Fr* d, const NttDomain& dom, bool inv, hipStream_t st) {
+void ntt_dif(Fr* d, const NttDomain& dom, bool inv, hipStream_t st, Prof* pf) {
   const uint32_t L = dom.log_n;
   if (L == 0) return;
+  const int ph = pf ? pf->begin(st, "ntt", (uint64_t)1 << L) : -1;
   const Fr* tw = (inv ? dom.itw : dom.tw).as<Fr>();
   // stages L-1 .. 0, top-down: choose pass sizes so that the last pass (s_lo = 0) is widest
   uint32_t s_hi = L;  // exclusive
@@ -99,11 +100,13 @@ void ntt_dif(Fr* d, const NttDomain& dom, bool inv, hipStream_t st) {
     run_pass(false, d, tw, L, s_lo, ns, st);
     s_hi = s_lo;
   }
+  if (pf) pf->end(st, ph);
 }
 
-void ntt_dit(Fr* d, const NttDomain& dom, bool inv, hipStream_t st) {
+void ntt_dit(Fr* d, const NttDomain& dom, bool inv, hipStream_t st, Prof* pf) {
   const uint32_t L = dom.log_n;
   if (L == 0) return;
+  const int ph = pf ? pf->begin(st, "ntt", (uint64_t)1 << L) : -1;
   const Fr* tw = (inv ? dom.itw : dom.tw).as<Fr>();
   uint32_t s_lo = 0;
   while (s_lo < L) {
@@ -111,6 +114,7 @@ void ntt_dit(Fr* d, const NttDomain& dom, bool inv, hipStream_t st) {
     run_pass(true, d, tw, L, s_lo, ns, st);
     s_lo += ns;
   }
+  if (pf) pf->end(st, ph);
 }
 
 // ------------------------------------------------------------ tables -----

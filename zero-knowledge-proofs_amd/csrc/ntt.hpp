@@ -33,8 +33,8 @@ struct NttDomain {
 void ntt_domain_init(NttDomain& d, uint32_t log_n, hipStream_t st);
 
 // In-place passes over n Montgomery Fr.
-void ntt_dif(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st);
-void ntt_dit(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st);
+void ntt_dif(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st, Prof* pf = nullptr);
+void ntt_dit(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st, Prof* pf = nullptr);
 
 // Elementwise helpers
 void fr_to_mont(const uint64_t* d_canon, Fr* d_out, size_t n, hipStream_t st);

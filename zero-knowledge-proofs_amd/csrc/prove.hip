@@ -137,6 +137,13 @@ __global__ void __launch_bounds__(256) k_gather_lo64(const uint64_t* __restrict_
   out[k] = src[(size_t)idx[k] * stride_words];
 }
 
+struct Extras {
+  uint64_t v[5];
+};
+__global__ void k_set_extras(uint64_t* __restrict__ dst, Extras e, uint32_t n) {
+  if (threadIdx.x < n) dst[threadIdx.x] = e.v[threadIdx.x];
+}
+
 // ------------------------------------------------------------- pk upload ---
 static uint64_t shard_lo(uint64_t len, uint32_t k, uint32_t ns) { return len * k / ns; }
 
@@ -293,23 +300,32 @@ static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipS
     m.val[k] = pk->csr.unit[k] ? nullptr : pk->csr.val[k].as<Fr>();
   }
   const uint64_t vrow = n > 1 ? 1 : 0;
+  Prof* pf = &ctx->prof;
+  int ph = pf->begin(st, "quotient_eval", n);
   k_csr_eval<<<ceil_div(n, 256), 256, 0, st>>>(m, reinterpret_cast<const Fr*>(d_z), pk->nc, pk->V, n, vrow,
                                                 ctx->qa.as<Fr>(), ctx->qb.as<Fr>(), ctx->qc.as<Fr>(),
                                                 ctx->flags.as<uint32_t>());
   ZK_LAUNCH_CHECK();
+  pf->end(st, ph);
   Fr* v[3] = {ctx->qa.as<Fr>(), ctx->qb.as<Fr>(), ctx->qc.as<Fr>()};
   for (int k = 0; k < 3; k++) {
-    ntt_dif(v[k], dom, /*inverse twiddles*/ true, st);                   // coefficients * n, bit-reversed
+    ntt_dif(v[k], dom, /*inverse twiddles*/ true, st, pf);               // coefficients * n, bit-reversed
+    ph = pf->begin(st, "quotient_misc", n);
     fr_scale_table(v[k], dom.gpow.as<Fr>(), pk->log_n, true, st);        // * n^-1 g^i
-    ntt_dit(v[k], dom, false, st);                                       // evaluations on g<w>, natural
+    pf->end(st, ph);
+    ntt_dit(v[k], dom, false, st, pf);                                   // evaluations on g<w>, natural
   }
+  ph = pf->begin(st, "quotient_misc", n);
   k_quot_pointwise<<<ceil_div(n, 256), 256, 0, st>>>(v[0], v[1], v[2], dom.zinv.as<Fr>(), n);
   ZK_LAUNCH_CHECK();
-  ntt_dif(v[0], dom, true, st);
+  pf->end(st, ph);
+  ntt_dif(v[0], dom, true, st, pf);
+  ph = pf->begin(st, "quotient_misc", n);
   ctx->scal[MSM_H].ensure(sizeof(uint64_t) * n);
   ctx->tmp_scal.ensure(sizeof(uint64_t) * n);
   k_h_final<<<ceil_div(n, 256), 256, 0, st>>>(v[0], dom.gipow.as<Fr>(), pk->log_n, ctx->tmp_scal.as<uint64_t>());
   ZK_LAUNCH_CHECK();
+  pf->end(st, ph);
 }
 
 static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, const zk_fr* r,
@@ -317,41 +333,55 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   hipStream_t st = ctx->stream;
   ctx->flags.ensure(16);
   ZK_HIP(hipMemsetAsync(ctx->flags.p, 0, 16, st));
-  quotient(ctx, pk, d_z, st);  // (Az, Bz, Cz) -> lo64(H) in tmp_scal
-  // scalars: lo64 of the assignment (or of H) gathered per compacted base, + extras
-  for (int slot = 0; slot < NUM_MSM; slot++) {
+  // The five MSMs are independent: each runs on its own stream.  A, B2, B1
+  // and IC need only z and start at once; H waits for the quotient, which
+  // runs on the main stream concurrently with them.  Latency-bound phases
+  // (scan, bucket reduction) of one MSM overlap the throughput-bound
+  // accumulation of another.
+  ZK_HIP(hipEventRecord(ctx->ev_scal, st));           // z (and flags reset) ready
+  auto launch_slot = [&](int slot) {
+    hipStream_t ss = ctx->side[slot];
     const uint32_t cnt = pk->count[slot], nex = pk->extras[slot];
     ctx->scal[slot].ensure(sizeof(uint64_t) * std::max<uint32_t>(cnt + nex, 1));
     if (cnt) {
       const uint64_t* src = slot == MSM_H ? ctx->tmp_scal.as<uint64_t>() : d_z;
       const int stride = slot == MSM_H ? 1 : 4;
-      k_gather_lo64<<<ceil_div(cnt, 256), 256, 0, st>>>(src, stride, pk->idx[slot].as<uint32_t>(), cnt,
+      k_gather_lo64<<<ceil_div(cnt, 256), 256, 0, ss>>>(src, stride, pk->idx[slot].as<uint32_t>(), cnt,
                                                          ctx->scal[slot].as<uint64_t>());
       ZK_LAUNCH_CHECK();
     }
     if (nex) {
-      uint64_t ex[5] = {1, 0, 0, 0, 0};
+      // scalar 1 for alpha_1 / beta_2 / beta_1, then the four u64 limbs of r (or s)
+      Extras ex{};
+      ex.v[0] = 1;
       const zk_fr* full = slot == MSM_A ? r : slot == MSM_B2 ? s : nullptr;
-      if (full) for (int k = 0; k < 4; k++) ex[1 + k] = full->l[k];
-      ZK_HIP(hipMemcpyAsync(ctx->scal[slot].as<uint64_t>() + cnt, ex, sizeof(uint64_t) * nex,
-                            hipMemcpyHostToDevice, st));
-      ZK_HIP(hipStreamSynchronize(st));  // ex is a stack buffer
+      if (full) for (int k = 0; k < 4; k++) ex.v[1 + k] = full->l[k];
+      k_set_extras<<<1, 64, 0, ss>>>(ctx->scal[slot].as<uint64_t>() + cnt, ex, nex);
+      ZK_LAUNCH_CHECK();
     }
+    const uint32_t n = cnt + nex;
+    if (slot == MSM_B2) {
+      msm_launch<G2>(ctx->msm[slot], pk->bases[slot].as<G2A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64, ss);
+      msm_download<G2>(ctx->msm[slot], ss);
+    } else {
+      msm_launch<G1>(ctx->msm[slot], pk->bases[slot].as<G1A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64, ss);
+      msm_download<G1>(ctx->msm[slot], ss);
+    }
+  };
+  // largest first: IC (3n), B2 (G2), A, B1
+  for (int slot : {MSM_IC, MSM_B2, MSM_A, MSM_B1}) {
+    ZK_HIP(hipStreamWaitEvent(ctx->side[slot], ctx->ev_scal, 0));
+    launch_slot(slot);
   }
-  for (int slot = 0; slot < NUM_MSM; slot++) {
-    const uint32_t n = pk->count[slot] + pk->extras[slot];
-    if (slot == MSM_B2)
-      msm_launch<G2>(ctx->msm[slot], pk->bases[slot].as<G2A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64, st);
-    else
-      msm_launch<G1>(ctx->msm[slot], pk->bases[slot].as<G1A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64, st);
-  }
+  quotient(ctx, pk, d_z, st);  // (Az, Bz, Cz) -> lo64(H) in tmp_scal
+  ZK_HIP(hipEventRecord(ctx->ev_quot, st));
+  ZK_HIP(hipStreamWaitEvent(ctx->side[MSM_H], ctx->ev_quot, 0));
+  launch_slot(MSM_H);
   uint32_t flags = 0;
   ZK_HIP(hipMemcpyAsync(&flags, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
-  for (int slot = 0; slot < NUM_MSM; slot++) {
-    if (slot == MSM_B2) msm_download<G2>(ctx->msm[slot], st);
-    else msm_download<G1>(ctx->msm[slot], st);
-  }
+  for (int slot = 0; slot < NUM_MSM; slot++) ZK_HIP(hipStreamSynchronize(ctx->side[slot]));
   ZK_HIP(hipStreamSynchronize(st));
+  ctx->prof.collect();
   Partial p{};
   p.status = ZK_OK;
   if (flags & 5u) p.status = ZK_ERR_INVALID_WITNESS;

@@ -36,18 +36,18 @@ struct FbTable {
 
 static host::X<host::Fq> g1_gen_host() {
   host::X<host::Fq> p;
-  std::memcpy(p.X_.l, G1_GEN_MONT, 48);
-  std::memcpy(p.Y.l, G1_GEN_MONT + 12, 48);
+  std::memcpy(p.X_.l, G1_GEN_HOSTM, 48);
+  std::memcpy(p.Y.l, G1_GEN_HOSTM + 12, 48);
   p.ZZ = host::one();
   p.ZZZ = host::one();
   return p;
 }
 static host::X<host::Fq2> g2_gen_host() {
   host::X<host::Fq2> p;
-  std::memcpy(p.X_.c0.l, G2_GEN_MONT, 48);
-  std::memcpy(p.X_.c1.l, G2_GEN_MONT + 12, 48);
-  std::memcpy(p.Y.c0.l, G2_GEN_MONT + 24, 48);
-  std::memcpy(p.Y.c1.l, G2_GEN_MONT + 36, 48);
+  std::memcpy(p.X_.c0.l, G2_GEN_HOSTM, 48);
+  std::memcpy(p.X_.c1.l, G2_GEN_HOSTM + 12, 48);
+  std::memcpy(p.Y.c0.l, G2_GEN_HOSTM + 24, 48);
+  std::memcpy(p.Y.c1.l, G2_GEN_HOSTM + 36, 48);
   p.ZZ = host::f_one<host::Fq2>();
   p.ZZZ = host::f_one<host::Fq2>();
   return p;
@@ -67,6 +67,8 @@ static void build_table(const host::X<HF>& G, std::vector<DA>& out) {
   for (int i = 0; i < 2048; i++) {
     HF x, y;
     if (!host::to_affine(pts[i], x, y)) { x = host::f_zero<HF>(); y = host::f_zero<HF>(); }
+    x = host::to_dev(x);   // device Montgomery radix (constants.hpp)
+    y = host::to_dev(y);
     static_assert(sizeof(HF) * 2 == sizeof(DA), "layout");
     std::memcpy(&out[i], &x, sizeof(HF));
     std::memcpy(reinterpret_cast<char*>(&out[i]) + sizeof(HF), &y, sizeof(HF));
@@ -358,7 +360,7 @@ int setup_impl(zk_ctx* ctx, const zk_r1cs_csr* q, const zk_setup_params* P, uint
   if (log_n > 32) return ZK_ERR_DOMAIN;
   if (V >= 0x80000000ull || n >= 0x80000000ull) return ZK_ERR_ARG;
 
-  auto to_dev = [](const host::Fr& h) { Fr d; std::memcpy(d.v, h.l, 32); return d; };
+  auto to_dev = [](const host::Fr& h) { Fr d; const host::Fr v = host::fr_to_dev(h); std::memcpy(d.v, v.l, 32); return d; };
   const host::Fr t = host::fr_from_u64(ta);
   host::Fr tn = t;
   for (uint32_t i = 0; i < log_n; i++) tn = host::fr_mul(tn, tn);

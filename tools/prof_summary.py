@@ -1,0 +1,89 @@
+"""Summarise rocprofv3 SQLite output (kernel trace and PMC passes) into the
+files committed under profiles/.
+
+  python tools/prof_summary.py trace <run_results.db> <out.md>
+  python tools/prof_summary.py pmc <fetch.db> <write.db> <out.json>
+
+PMC correction (MI355X_MICROARCH.md, HBM): on gfx950 FETCH_SIZE reports half
+the bytes of wide coalesced reads, so traffic = 2*FETCH_SIZE + WRITE_SIZE
+(both in KiB per dispatch).  Our gathers of 96/192-byte points are not the
+calibrated access shape; the doubled figure is an upper estimate.
+"""
+import json
+import sqlite3
+import sys
+
+
+def short(name):
+    n = name.replace(".kd", "")
+    for pre in ("_ZN2zk", "_Z"):
+        if n.startswith(pre):
+            n = n[len(pre):]
+    i = 0
+    while i < len(n) and n[i].isdigit():
+        i += 1
+    ln = int(n[:i]) if i else 0
+    base = n[i:i + ln] if ln else n
+    rest = n[i + ln:]
+    tag = ""
+    if "G1" in rest:
+        tag = "<G1>"
+    elif "G2" in rest:
+        tag = "<G2>"
+    elif rest.startswith("ILb1") or rest.startswith("ILi1ELb1") or rest.startswith("ILi4ELb1"):
+        tag = "<scatter>" if "digits" in base else "<dit>"
+    elif rest.startswith("ILb0") or rest.startswith("ILi1ELb0") or rest.startswith("ILi4ELb0"):
+        tag = "<count>" if "digits" in base else "<dif>"
+    return base + tag
+
+
+def trace(db, out):
+    cur = sqlite3.connect(db).cursor()
+    rows = cur.execute("""select s.kernel_name, count(*), sum(d.end-d.start), avg(d.end-d.start),
+                          min(d.end-d.start), max(d.end-d.start)
+                          from rocpd_kernel_dispatch d join rocpd_info_kernel_symbol s on d.kernel_id = s.id
+                          group by s.kernel_name order by 3 desc""").fetchall()
+    total = sum(r[2] for r in rows)
+    lines = ["| kernel | calls | total ms | avg us | min us | max us | % |", "|---|---|---|---|---|---|---|"]
+    for name, n, tot, avg, mn, mx in rows:
+        lines.append("| %s | %d | %.3f | %.1f | %.1f | %.1f | %.1f |" % (
+            short(name), n, tot / 1e6, avg / 1e3, mn / 1e3, mx / 1e3, 100.0 * tot / total))
+    open(out, "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines[:20]))
+
+
+def pmc_per_kernel(db, counter):
+    cur = sqlite3.connect(db).cursor()
+    q = f"""select s.kernel_name, count(*), avg(e.value)
+            from rocpd_pmc_event e
+            join rocpd_info_pmc p on e.pmc_id = p.id
+            join rocpd_kernel_dispatch d on d.event_id = e.event_id
+            join rocpd_info_kernel_symbol s on d.kernel_id = s.id
+            where p.name = '{counter}' group by s.kernel_name"""
+    return {short(r[0]): (r[1], r[2]) for r in cur.execute(q).fetchall()}
+
+
+def pmc(fetch_db, write_db, out):
+    f = pmc_per_kernel(fetch_db, "FETCH_SIZE")
+    w = pmc_per_kernel(write_db, "WRITE_SIZE")
+    kernels = {}
+    for k in sorted(set(f) | set(w)):
+        fk = f.get(k, (0, 0.0))[1]
+        wk = w.get(k, (0, 0.0))[1]
+        kernels[k] = {"fetch_kib": round(fk, 1), "write_kib": round(wk, 1),
+                      "traffic_bytes_per_launch": int((2 * fk + wk) * 1024)}
+    acc = [kernels[k] for k in kernels if k.startswith("k_msm_accum")]
+    res = {"note": "traffic = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch (gfx950 FETCH correction)",
+           "kernels": kernels}
+    if acc:
+        res["msm_accum_bytes_per_launch"] = int(sum(a["traffic_bytes_per_launch"] for a in acc) / len(acc))
+    json.dump(res, open(out, "w"), indent=1)
+    for k, v in kernels.items():
+        print(k, v)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "trace":
+        trace(sys.argv[2], sys.argv[3])
+    else:
+        pmc(sys.argv[2], sys.argv[3], sys.argv[4])

@@ -51,8 +51,11 @@ zk_ctx* zk_ctx_create(int device) {
     std::unique_ptr<zk_ctx> c(new zk_ctx());
     c->device = device;
     for (int i = 0; i < NUM_MSM; i++) c->msm[i].prof = &c->prof;
-    ZK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    for (int i = 0; i < NUM_MSM; i++) ZK_HIP(hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking));
+    int lo_prio = 0, hi_prio = 0;
+    ZK_HIP(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
+    ZK_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio));   // quotient + H
+    ZK_HIP(hipStreamCreateWithPriority(&c->side[0], hipStreamNonBlocking, hi_prio));  // G2 MSM
+    for (int i = 1; i < NUM_SIDE; i++) ZK_HIP(hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking, lo_prio));
     ZK_HIP(hipEventCreateWithFlags(&c->ev_quot, hipEventDisableTiming));
     ZK_HIP(hipEventCreateWithFlags(&c->ev_scal, hipEventDisableTiming));
     return c.release();
@@ -65,9 +68,9 @@ void zk_ctx_destroy(zk_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
-  for (int i = 0; i < NUM_MSM; i++) (void)hipStreamSynchronize(ctx->side[i]);
+  for (int i = 0; i < NUM_SIDE; i++) (void)hipStreamSynchronize(ctx->side[i]);
   ctx->domains.clear();
-  for (int i = 0; i < NUM_MSM; i++) (void)hipStreamDestroy(ctx->side[i]);
+  for (int i = 0; i < NUM_SIDE; i++) (void)hipStreamDestroy(ctx->side[i]);
   (void)hipStreamDestroy(ctx->stream);
   (void)hipEventDestroy(ctx->ev_quot);
   (void)hipEventDestroy(ctx->ev_scal);

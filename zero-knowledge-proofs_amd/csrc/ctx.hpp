@@ -12,6 +12,7 @@
 namespace zk {
 
 constexpr int NUM_MSM = 5;  // pi_A (G1), pi_B (G2), B1 (G1), IC (G1), H (G1)
+constexpr int NUM_SIDE = 3; // side streams (+ main = 4 = GPU_MAX_HW_QUEUES)
 enum MsmSlot { MSM_A = 0, MSM_B2 = 1, MSM_B1 = 2, MSM_IC = 3, MSM_H = 4 };
 
 // Device copy of the constraint matrices (the QAP in sparse form).
@@ -26,7 +27,7 @@ struct CsrDev {
 struct zk_ctx {
   int device = 0;
   hipStream_t stream = nullptr;                 // main stream
-  hipStream_t side[zk::NUM_MSM] = {};           // one stream per proof MSM
+  hipStream_t side[zk::NUM_SIDE] = {};          // G2 / IC / A+B1 MSM streams
   hipEvent_t ev_quot = nullptr, ev_scal = nullptr;
   std::string err;
   zk::MsmWork msm[zk::NUM_MSM];

@@ -13,6 +13,11 @@
 #pragma once
 #include "ff.hpp"
 
+// Scheduling barrier between field operations: keeps the scheduler from
+// overlapping independent multiplies (each holds ~60 VGPRs of 28-bit limbs),
+// which otherwise pushes G2 formulas past 512 VGPRs into scratch.
+#define ZK_SB() __builtin_amdgcn_sched_barrier(0)
+
 template <class F>
 struct Affine {
   F x, y;
@@ -51,15 +56,23 @@ template <class F>
 ZK_DI XYZZ<F> xyzz_dbl(const XYZZ<F>& p) {
   F U = f_add(p.Y, p.Y);
   F V = f_sqr(U);
+  ZK_SB();
   F W = f_mul(U, V);
+  ZK_SB();
   F S = f_mul(p.X, V);
+  ZK_SB();
   F X2 = f_sqr(p.X);
+  ZK_SB();
   F M = f_add(f_add(X2, X2), X2);
   XYZZ<F> r;
   r.X = f_sub(f_sqr(M), f_add(S, S));
+  ZK_SB();
   r.Y = f_sub(f_mul(M, f_sub(S, r.X)), f_mul(W, p.Y));
+  ZK_SB();
   r.ZZ = f_mul(V, p.ZZ);
+  ZK_SB();
   r.ZZZ = f_mul(W, p.ZZZ);
+  ZK_SB();
   return r;   // p at infinity (ZZ = 0) stays at infinity
 }
 
@@ -68,13 +81,19 @@ template <class F>
 ZK_DI XYZZ<F> aff_dbl(const Affine<F>& a) {
   F U = f_add(a.y, a.y);
   F V = f_sqr(U);
+  ZK_SB();
   F W = f_mul(U, V);
+  ZK_SB();
   F S = f_mul(a.x, V);
+  ZK_SB();
   F X2 = f_sqr(a.x);
+  ZK_SB();
   F M = f_add(f_add(X2, X2), X2);
   XYZZ<F> r;
   r.X = f_sub(f_sqr(M), f_add(S, S));
+  ZK_SB();
   r.Y = f_sub(f_mul(M, f_sub(S, r.X)), f_mul(W, a.y));
+  ZK_SB();
   r.ZZ = V;
   r.ZZZ = W;
   return r;
@@ -85,7 +104,9 @@ template <class F>
 ZK_DI XYZZ<F> xyzz_madd(const XYZZ<F>& p, const Affine<F>& a) {
   if (xyzz_is_inf(p)) return xyzz_from_aff(a);
   F U2 = f_mul(a.x, p.ZZ);
+  ZK_SB();
   F S2 = f_mul(a.y, p.ZZZ);
+  ZK_SB();
   F P = f_sub(U2, p.X);
   F R = f_sub(S2, p.Y);
   if (f_is_zero(P)) {
@@ -93,13 +114,20 @@ ZK_DI XYZZ<F> xyzz_madd(const XYZZ<F>& p, const Affine<F>& a) {
     XYZZ<F> r; xyzz_set_inf(r); return r;
   }
   F PP = f_sqr(P);
+  ZK_SB();
   F PPP = f_mul(P, PP);
+  ZK_SB();
   F Q = f_mul(p.X, PP);
+  ZK_SB();
   XYZZ<F> r;
   r.X = f_sub(f_sub(f_sqr(R), PPP), f_add(Q, Q));
+  ZK_SB();
   r.Y = f_sub(f_mul(R, f_sub(Q, r.X)), f_mul(p.Y, PPP));
+  ZK_SB();
   r.ZZ = f_mul(p.ZZ, PP);
+  ZK_SB();
   r.ZZZ = f_mul(p.ZZZ, PPP);
+  ZK_SB();
   return r;
 }
 
@@ -109,9 +137,13 @@ ZK_DI XYZZ<F> xyzz_add(const XYZZ<F>& p, const XYZZ<F>& q) {
   if (xyzz_is_inf(p)) return q;
   if (xyzz_is_inf(q)) return p;
   F U1 = f_mul(p.X, q.ZZ);
+  ZK_SB();
   F U2 = f_mul(q.X, p.ZZ);
+  ZK_SB();
   F S1 = f_mul(p.Y, q.ZZZ);
+  ZK_SB();
   F S2 = f_mul(q.Y, p.ZZZ);
+  ZK_SB();
   F P = f_sub(U2, U1);
   F R = f_sub(S2, S1);
   if (f_is_zero(P)) {
@@ -119,13 +151,20 @@ ZK_DI XYZZ<F> xyzz_add(const XYZZ<F>& p, const XYZZ<F>& q) {
     XYZZ<F> r; xyzz_set_inf(r); return r;
   }
   F PP = f_sqr(P);
+  ZK_SB();
   F PPP = f_mul(P, PP);
+  ZK_SB();
   F Q = f_mul(U1, PP);
+  ZK_SB();
   XYZZ<F> r;
   r.X = f_sub(f_sub(f_sqr(R), PPP), f_add(Q, Q));
+  ZK_SB();
   r.Y = f_sub(f_mul(R, f_sub(Q, r.X)), f_mul(S1, PPP));
+  ZK_SB();
   r.ZZ = f_mul(f_mul(p.ZZ, q.ZZ), PP);
+  ZK_SB();
   r.ZZZ = f_mul(f_mul(p.ZZZ, q.ZZZ), PPP);
+  ZK_SB();
   return r;
 }
 

@@ -237,16 +237,23 @@ ZK_DI bool fq2_is_zero(const Fq2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c
 ZK_DI Fq2 fq2_add(const Fq2& a, const Fq2& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
 ZK_DI Fq2 fq2_sub(const Fq2& a, const Fq2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
 ZK_DI Fq2 fq2_neg(const Fq2& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
+// sched_barrier between the three independent products keeps the scheduler
+// from interleaving them (3x the live 28-bit limb sets -> spills in G2).
 ZK_DI Fq2 fq2_mul(const Fq2& a, const Fq2& b) {
   Fq t0 = fq_mul(a.c0, b.c0);
+  __builtin_amdgcn_sched_barrier(0);
   Fq t1 = fq_mul(a.c1, b.c1);
+  __builtin_amdgcn_sched_barrier(0);
   Fq m = fq_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  __builtin_amdgcn_sched_barrier(0);
   return {fp_sub(t0, t1), fp_sub(fp_sub(m, t0), t1)};
 }
 ZK_DI Fq2 fq2_sqr(const Fq2& a) {
   // (c0 + c1 u)^2 = (c0+c1)(c0-c1) + 2 c0 c1 u
   Fq m = fq_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  __builtin_amdgcn_sched_barrier(0);
   Fq t = fq_mul(a.c0, a.c1);
+  __builtin_amdgcn_sched_barrier(0);
   return {m, fp_add(t, t)};
 }
 ZK_DI Fq2 fq2_inv(const Fq2& a) {

@@ -333,14 +333,18 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   hipStream_t st = ctx->stream;
   ctx->flags.ensure(16);
   ZK_HIP(hipMemsetAsync(ctx->flags.p, 0, 16, st));
-  // The five MSMs are independent: each runs on its own stream.  A, B2, B1
-  // and IC need only z and start at once; H waits for the quotient, which
-  // runs on the main stream concurrently with them.  Latency-bound phases
-  // (scan, bucket reduction) of one MSM overlap the throughput-bound
-  // accumulation of another.
+  // The five MSMs are independent.  Streams (<= GPU_MAX_HW_QUEUES = 4, so no
+  // two share a hardware queue): main (high priority) runs the quotient and
+  // then the H MSM that depends on it; side[0] (high priority) the G2 MSM,
+  // the longest chain; side[1] the IC MSM (3n bases); side[2] A then B1.
+  // Latency-bound phases (scan, bucket reduction) of one MSM overlap the
+  // throughput-bound accumulation of another.
   ZK_HIP(hipEventRecord(ctx->ev_scal, st));           // z (and flags reset) ready
+  auto stream_of = [&](int slot) {
+    return slot == MSM_H ? st : slot == MSM_B2 ? ctx->side[0] : slot == MSM_IC ? ctx->side[1] : ctx->side[2];
+  };
   auto launch_slot = [&](int slot) {
-    hipStream_t ss = ctx->side[slot];
+    hipStream_t ss = stream_of(slot);
     const uint32_t cnt = pk->count[slot], nex = pk->extras[slot];
     ctx->scal[slot].ensure(sizeof(uint64_t) * std::max<uint32_t>(cnt + nex, 1));
     if (cnt) {
@@ -368,18 +372,13 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       msm_download<G1>(ctx->msm[slot], ss);
     }
   };
-  // largest first: IC (3n), B2 (G2), A, B1
-  for (int slot : {MSM_IC, MSM_B2, MSM_A, MSM_B1}) {
-    ZK_HIP(hipStreamWaitEvent(ctx->side[slot], ctx->ev_scal, 0));
-    launch_slot(slot);
-  }
-  quotient(ctx, pk, d_z, st);  // (Az, Bz, Cz) -> lo64(H) in tmp_scal
-  ZK_HIP(hipEventRecord(ctx->ev_quot, st));
-  ZK_HIP(hipStreamWaitEvent(ctx->side[MSM_H], ctx->ev_quot, 0));
+  for (int k = 0; k < NUM_SIDE; k++) ZK_HIP(hipStreamWaitEvent(ctx->side[k], ctx->ev_scal, 0));
+  for (int slot : {MSM_B2, MSM_IC, MSM_A, MSM_B1}) launch_slot(slot);
+  quotient(ctx, pk, d_z, st);  // (Az, Bz, Cz) -> lo64(H) in tmp_scal, then H on the same stream
   launch_slot(MSM_H);
   uint32_t flags = 0;
   ZK_HIP(hipMemcpyAsync(&flags, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
-  for (int slot = 0; slot < NUM_MSM; slot++) ZK_HIP(hipStreamSynchronize(ctx->side[slot]));
+  for (int k = 0; k < NUM_SIDE; k++) ZK_HIP(hipStreamSynchronize(ctx->side[k]));
   ZK_HIP(hipStreamSynchronize(st));
   ctx->prof.collect();
   Partial p{};

@@ -92,18 +92,68 @@ def test_msm_g2_random_vs_oracle(ctx, oracle, n, bits):
     assert np.array_equal(ctx.msm_g2(bases, sc, bits), oracle.msm_g2(bases, sc))
 
 
-def test_msm_g1_linearity_large(ctx, oracle):
-    """Size-independent property at 2^16: bases (a + i b) G give
-    G * (a sum s_i + b sum i s_i)."""
-    R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
-    n, a, b = 1 << 16, 0xDEADBEEF, 0xC0FFEE
+R_MOD = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+LIN_A, LIN_B = 0xDEADBEEF, 0xC0FFEE
+
+
+@pytest.fixture(scope="module")
+def lin_bases(oracle):
+    """2^16 bases (a + i b) G, built incrementally."""
+    n = 1 << 16
     g = oracle.g1_generator()
-    step = oracle.g1_mul(g, b)
+    step = oracle.g1_mul(g, LIN_B)
     bases = np.empty((n, 13), dtype=np.uint64)
-    bases[0] = oracle.g1_mul(g, a)
+    bases[0] = oracle.g1_mul(g, LIN_A)
     for i in range(1, n):
         bases[i] = oracle.g1_add(bases[i - 1], step)
-    sc = oracle.random_fr(n, 0x5EED0001)
+    return bases
+
+
+def _closed_form(oracle, sc):
     s = oracle.fr_ints(sc)
-    k = (a * sum(s) + b * sum(i * x for i, x in enumerate(s))) % R
-    assert np.array_equal(ctx.msm_g1(bases, sc, 255), oracle.g1_mul(g, k))
+    k = (LIN_A * sum(s) + LIN_B * sum(i * x for i, x in enumerate(s))) % R_MOD
+    return oracle.g1_mul(oracle.g1_generator(), k)
+
+
+def test_msm_g1_linearity_large(ctx, oracle, lin_bases):
+    """Size-independent property at 2^16: bases (a + i b) G give
+    G * (a sum s_i + b sum i s_i)."""
+    sc = oracle.random_fr(len(lin_bases), 0x5EED0001)
+    assert np.array_equal(ctx.msm_g1(lin_bases, sc, 255), _closed_form(oracle, sc))
+
+
+@pytest.mark.parametrize("pattern", ["ones", "bits", "two_bits", "one_value", "sparse_big"])
+@pytest.mark.parametrize("bits", [64, 255])
+def test_msm_g1_skewed_scalars(ctx, oracle, lin_bases, pattern, bits):
+    """Witness-like scalar distributions: most scalars 0/1 put 2^16 entries
+    into one bucket, which the segmented merge must finish at log depth."""
+    n = len(lin_bases)
+    rng = np.random.default_rng(5)
+    sc = np.zeros((n, 4), dtype=np.uint64)
+    if pattern == "ones":
+        sc[:, 0] = 1
+    elif pattern == "bits":
+        sc[:, 0] = rng.integers(0, 2, n, dtype=np.uint64)
+    elif pattern == "two_bits":
+        sc[:, 0] = rng.integers(0, 4, n, dtype=np.uint64)
+    elif pattern == "one_value":
+        sc[:] = oracle.random_fr(1, 9)[0]
+        if bits == 64:
+            sc[:, 1:] = 0
+    else:
+        sc[:, 0] = rng.integers(0, 2, n, dtype=np.uint64)
+        idx = rng.choice(n, 64, replace=False)
+        big = oracle.random_fr(64, 10)
+        if bits == 64:
+            big[:, 1:] = 0
+        sc[idx] = big
+    assert np.array_equal(ctx.msm_g1(lin_bases, sc, bits), _closed_form(oracle, sc))
+
+
+@pytest.mark.parametrize("pattern", ["ones", "two_bits"])
+def test_msm_g2_skewed_scalars(ctx, oracle, pattern):
+    n = 4096
+    bases = np.repeat(_g2_bases(oracle, 16, 99), n // 16, axis=0)
+    sc = np.zeros((n, 4), dtype=np.uint64)
+    sc[:, 0] = 1 if pattern == "ones" else np.random.default_rng(3).integers(0, 4, n, dtype=np.uint64)
+    assert np.array_equal(ctx.msm_g2(bases, sc, 64), oracle.msm_g2(bases, sc))

@@ -33,7 +33,7 @@ __device__ __forceinline__ Fq mul_v2(const Fq& a, const Fq& b) {
       hprev = (uint32_t)(Pj >> 32);
     }
     uint32_t top = hprev + cc;
-    const uint32_t m = (uint32_t)T[0] * FqParams::INV;
+    const uint32_t m = (uint32_t)T[0] * 0xfffcfffdu;  // -p^-1 mod 2^32
     uint64_t Q = (uint64_t)m * FqParams::MOD[0] + T[0];
     hprev = (uint32_t)(Q >> 32);
     cc = 0;
@@ -97,7 +97,9 @@ __device__ __forceinline__ F28 mul_r28(const F28& a, const F28& b) {
 
 template <int V>
 __global__ void __launch_bounds__(256) kbench(const uint32_t* in, uint32_t* out, int iters) {
+  extern __shared__ uint32_t pad[];   // latency mode: a large dynamic LDS request caps one block per CU
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (iters < 0) pad[threadIdx.x] = 0;
   if (V <= 2) {
     Fq x, y;
     for (int i = 0; i < 12; i++) { x.v[i] = in[(t % 1024) * 24 + i]; y.v[i] = in[(t % 1024) * 24 + 12 + i]; }
@@ -148,21 +150,29 @@ int main() {
   hipEvent_t a, b;
   CHK(hipEventCreate(&a));
   CHK(hipEventCreate(&b));
-  const char* names[4] = {"v1 CIOS rolled", "v2 CIOS addc", "r28 comba 1acc", "r28 comba 2acc"};
-  for (int v = 1; v <= 4; v++) {
-    for (int rep = 0; rep < 2; rep++) {
-      CHK(hipEventRecord(a));
-      switch (v) {
-        case 1: kbench<1><<<threads / 256, 256>>>(d32, dout, iters); break;
-        case 2: kbench<2><<<threads / 256, 256>>>(d32, dout, iters); break;
-        case 3: kbench<3><<<threads / 256, 256>>>(d28, dout, iters); break;
-        case 4: kbench<4><<<threads / 256, 256>>>(d28, dout, iters); break;
+  const char* names[4] = {"fp_mul (ff.hpp)", "v2 CIOS addc", "r28 comba 1acc", "r28 comba 2acc"};
+  // mode 0: full occupancy; mode 1: one 256-thread block per CU (1 wave/SIMD), latency-bound
+  for (int mode = 0; mode < 2; mode++) {
+    const int nthr = mode ? 256 * 256 : threads;
+    const size_t lds = mode ? 96 * 1024 : 0;
+    const int it = mode ? iters / 4 : iters;
+    for (int v = 1; v <= 4; v++) {
+      for (int rep = 0; rep < 2; rep++) {
+        CHK(hipEventRecord(a));
+        switch (v) {
+          case 1: kbench<1><<<nthr / 256, 256, lds>>>(d32, dout, it); break;
+          case 2: kbench<2><<<nthr / 256, 256, lds>>>(d32, dout, it); break;
+          case 3: kbench<3><<<nthr / 256, 256, lds>>>(d28, dout, it); break;
+          case 4: kbench<4><<<nthr / 256, 256, lds>>>(d28, dout, it); break;
+        }
+        CHK(hipEventRecord(b));
+        CHK(hipEventSynchronize(b));
+        float ms;
+        CHK(hipEventElapsedTime(&ms, a, b));
+        if (rep)
+          printf("%s %-18s %8.2f ms  %8.2f Gmul/s  %6.0f ns/mul/thread\n", mode ? "1wave/SIMD" : "full      ",
+                 names[v - 1], ms, (double)nthr * it / ms / 1e6, ms * 1e6 / it);
       }
-      CHK(hipEventRecord(b));
-      CHK(hipEventSynchronize(b));
-      float ms;
-      CHK(hipEventElapsedTime(&ms, a, b));
-      if (rep) printf("%-18s %8.2f ms  %8.2f Gmul/s\n", names[v - 1], ms, (double)threads * iters / ms / 1e6);
     }
   }
   return 0;

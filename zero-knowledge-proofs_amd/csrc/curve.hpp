@@ -76,6 +76,11 @@ ZK_DI XYZZ<F> xyzz_dbl(const XYZZ<F>& p) {
   return r;   // p at infinity (ZZ = 0) stays at infinity
 }
 
+// Out-of-line doubling for the (rare) p == q branch of xyzz_add: inlined, its
+// live set adds to the add's and pushes G2 into scratch.
+template <class F>
+__device__ __noinline__ XYZZ<F> xyzz_dbl_call(const XYZZ<F>& p) { return xyzz_dbl(p); }
+
 // mdbl-2008-s-1: 2*a for affine a (not infinity)
 template <class F>
 ZK_DI XYZZ<F> aff_dbl(const Affine<F>& a) {
@@ -131,39 +136,45 @@ ZK_DI XYZZ<F> xyzz_madd(const XYZZ<F>& p, const Affine<F>& a) {
   return r;
 }
 
-// add-2008-s: p + q
+// add-2008-s: p + q.  Operations are ordered so that each input coordinate
+// dies as early as possible (G2 points are 96 VGPRs each; the textbook order
+// keeps both points and four products live at once and spills).
 template <class F>
 ZK_DI XYZZ<F> xyzz_add(const XYZZ<F>& p, const XYZZ<F>& q) {
   if (xyzz_is_inf(p)) return q;
   if (xyzz_is_inf(q)) return p;
   F U1 = f_mul(p.X, q.ZZ);
   ZK_SB();
-  F U2 = f_mul(q.X, p.ZZ);
+  F P = f_sub(f_mul(q.X, p.ZZ), U1);
   ZK_SB();
   F S1 = f_mul(p.Y, q.ZZZ);
   ZK_SB();
-  F S2 = f_mul(q.Y, p.ZZZ);
+  F R = f_sub(f_mul(q.Y, p.ZZZ), S1);
   ZK_SB();
-  F P = f_sub(U2, U1);
-  F R = f_sub(S2, S1);
   if (f_is_zero(P)) {
-    if (f_is_zero(R)) return xyzz_dbl(p);
+    if (f_is_zero(R)) return xyzz_dbl_call(p);
     XYZZ<F> r; xyzz_set_inf(r); return r;
   }
+  XYZZ<F> r;
   F PP = f_sqr(P);
+  ZK_SB();
+  r.ZZ = f_mul(p.ZZ, q.ZZ);
+  ZK_SB();
+  r.ZZ = f_mul(r.ZZ, PP);
   ZK_SB();
   F PPP = f_mul(P, PP);
   ZK_SB();
+  r.ZZZ = f_mul(p.ZZZ, q.ZZZ);
+  ZK_SB();
+  r.ZZZ = f_mul(r.ZZZ, PPP);
+  ZK_SB();
   F Q = f_mul(U1, PP);
   ZK_SB();
-  XYZZ<F> r;
   r.X = f_sub(f_sub(f_sqr(R), PPP), f_add(Q, Q));
   ZK_SB();
-  r.Y = f_sub(f_mul(R, f_sub(Q, r.X)), f_mul(S1, PPP));
+  F T = f_mul(S1, PPP);
   ZK_SB();
-  r.ZZ = f_mul(f_mul(p.ZZ, q.ZZ), PP);
-  ZK_SB();
-  r.ZZZ = f_mul(f_mul(p.ZZZ, q.ZZZ), PPP);
+  r.Y = f_sub(f_mul(R, f_sub(Q, r.X)), T);
   ZK_SB();
   return r;
 }

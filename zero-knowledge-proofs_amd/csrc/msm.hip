@@ -1,6 +1,7 @@
 // msm.hip -- Pippenger bucket MSM kernels for gfx950 (see msm.hpp for the
 // pipeline).  Wave64 throughout; no MFMA (big-integer modular arithmetic).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -26,9 +27,12 @@ MsmPlan msm_make_plan(uint32_t n, int bits, int sw, int force_c) {
     if (cost < best) { best = cost; best_c = c; }
   }
   if (force_c) best_c = force_c;
+  // tuning overrides (tools/phase_bench.py sweeps): ZK_MSM_C, ZK_MSM_K
+  if (const char* e = getenv("ZK_MSM_C")) best_c = std::max(4, std::min(16, atoi(e)));
   p.c = best_c;
   p.nwin = (bits + p.c - 1) / p.c;
   p.K = 32;
+  if (const char* e = getenv("ZK_MSM_K")) p.K = std::max(1, atoi(e));
   uint32_t G = 0, rc = 0, q = 0;
   for (int w = 0; w < p.nwin; w++) {
     const int width = (w == p.nwin - 1) ? bits - p.c * w : p.c;
@@ -77,8 +81,9 @@ __global__ void __launch_bounds__(256) k_msm_digits(const uint64_t* __restrict__
                                                     uint32_t* __restrict__ cursor,
                                                     uint32_t* __restrict__ ent,
                                                     uint32_t* __restrict__ key) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= p.n) return;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = (int)(threadIdx.x & 63);
+  if (i >= p.n) return;   // whole trailing lanes only: the ballots below see the live ones
   uint64_t s[SW];
 #pragma unroll
   for (int k = 0; k < SW; k++) s[k] = sc[(size_t)i * SW + k];
@@ -98,15 +103,28 @@ __global__ void __launch_bounds__(256) k_msm_digits(const uint64_t* __restrict__
       mag = v;
       carry = 0;
     }
-    if (mag) {
-      uint32_t g = p.boff[w] + mag - 1;
-      if (!SCATTER) {
-        atomicAdd(&counts[g], 1u);
-      } else {
-        uint32_t pos = atomicAdd(&cursor[g], 1u);
+    // Wave-aggregated atomics: the lanes sharing the first active lane's
+    // bucket take one atomic between them.  Skewed scalars (a witness of
+    // mostly ones) otherwise serialise ~n atomics on a single counter.
+    const uint32_t gg = mag ? p.boff[w] + mag - 1 : 0xffffffffu;
+    const uint32_t lead = __builtin_amdgcn_readfirstlane(gg);
+    const uint64_t same = __ballot(gg == lead);
+    const int lead_lane = __builtin_ctzll(same);
+    const bool agg = lead != 0xffffffffu && gg == lead;
+    uint32_t base = 0;
+    if (agg && lane == lead_lane)
+      base = atomicAdd(SCATTER ? &cursor[lead] : &counts[lead], (uint32_t)__builtin_popcountll(same));
+    if (SCATTER) {
+      base = __shfl(base, lead_lane);
+      uint32_t pos;
+      if (agg) pos = base + (uint32_t)__builtin_popcountll(same & ((1ull << lane) - 1));
+      else if (gg != 0xffffffffu) pos = atomicAdd(&cursor[gg], 1u);
+      if (gg != 0xffffffffu) {
         ent[pos] = i | (neg ? 0x80000000u : 0u);
-        key[pos] = g;
+        key[pos] = gg;
       }
+    } else if (!agg && gg != 0xffffffffu) {
+      atomicAdd(&counts[gg], 1u);
     }
   }
 }
@@ -155,7 +173,7 @@ __global__ void __launch_bounds__(1024) k_scan_part(uint32_t* __restrict__ part,
   }
   if (t < nblk) part[t] = sh[t] - v;
 }
-__global__ void __launch_bounds__(256) k_scan_down(const uint32_t* __restrict__ counts, uint32_t G,
+__global__ void __launch_bounds__(256) k_scan_down(uint32_t* __restrict__ counts, uint32_t G,
                                                    const uint32_t* __restrict__ part, uint32_t* __restrict__ off,
                                                    uint32_t* __restrict__ cur) {
   __shared__ uint32_t sh[256];
@@ -164,6 +182,7 @@ __global__ void __launch_bounds__(256) k_scan_down(const uint32_t* __restrict__ 
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     c[k] = base + k < G ? counts[base + k] : 0;
+    if (base + k < G) counts[base + k] = 0;   // ready for the next MSM on this workspace
     s += c[k];
   }
   uint32_t tot;
@@ -228,9 +247,30 @@ __global__ void __launch_bounds__(128) k_msm_accum(const typename C::A* __restri
   else st_vec(&buckets[cur], acc);
 }
 
-// Buckets whose entries span several threads: tail(t0) + head(t0+1..t1).
+// Buckets whose entries span several accumulate chunks.  A bucket over
+// P = t1 - t0 + 1 chunks is tail(t0) + head(t0+1) + ... + head(t1):
+//  * P <= MSM_FIX_MAX (the common case: ~1-2): one thread sums the pieces
+//    serially (k_msm_fixup), all such buckets at once;
+//  * larger P (skewed scalars: a witness of mostly ones puts ~n entries in
+//    one bucket) goes through a log-depth segmented merge (k_msm_merge):
+//    level l covers entry ranges ("groups") of W = K 4^l; a group's children
+//    are the 4 groups of level l-1 (level 0 = the chunks), and each leaves at
+//    most two open pieces of a large bucket --
+//      first slot  the bucket holding entry s, if it began before s
+//      last slot   the bucket holding entry e-1, if it began in [s, e) and
+//                  continues past e
+//    both decidable from the sorted keys and bucket offsets alone.  A level
+//    reads its children's <= 8 slots in key order, writes buckets that are
+//    now complete and passes the rest up: log4(M/K) levels of <= 7 adds.
+constexpr uint32_t MSM_FIX_MAX = 4;
+constexpr int MSM_MERGE_FAN = 4;
+
+__device__ __forceinline__ bool big_bucket(const uint32_t* off, uint32_t b, uint32_t K) {
+  return (off[b + 1] - 1) / K - off[b] / K + 1 > MSM_FIX_MAX;
+}
+
 template <class C>
-__global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ off, uint32_t G, int K,
+__global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ off, uint32_t G, uint32_t K,
                                                    typename C::X* __restrict__ buckets,
                                                    const typename C::X* __restrict__ partials) {
   using X = typename C::X;
@@ -239,37 +279,82 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
   const uint32_t bs = off[g], be = off[g + 1];
   if (be == bs) return;
   const uint32_t t0 = bs / K, t1 = (be - 1) / K;
-  if (t0 == t1) return;
+  if (t0 == t1 || t1 - t0 + 1 > MSM_FIX_MAX) return;
   X acc = ld_vec(&partials[2 * (size_t)t0 + 1]);
   for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, ld_vec(&partials[2 * (size_t)t]));
   st_vec(&buckets[g], acc);
 }
 
-// ------------------------------------------------------------- reduce ---
-// Workgroup-wide plain sum of one XYZZ per thread (tree over the first
-// `len` threads' values; the result lands in sh[0]).
-template <class X>
-__device__ __forceinline__ void tree_sum(X* sh, X v, uint32_t len) {
-  const uint32_t t = threadIdx.x;
-  sh[t] = v;
-  __syncthreads();
-  uint32_t p2 = 1;
-  while (p2 < len) p2 <<= 1;
-  for (uint32_t d = p2 >> 1; d > 0; d >>= 1) {
-    if (t < d && t + d < len) sh[t] = xyzz_add(sh[t], sh[t + d]);
-    __syncthreads();
+template <class C>
+__global__ void __launch_bounds__(128) k_msm_merge(const uint32_t* __restrict__ key,
+                                                   const uint32_t* __restrict__ off, uint32_t G, uint32_t K,
+                                                   uint64_t W, typename C::X* __restrict__ buckets,
+                                                   const typename C::X* __restrict__ in,
+                                                   typename C::X* __restrict__ out) {
+  using X = typename C::X;
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t M = off[G];
+  const uint64_t s64 = (uint64_t)u * W;
+  if (s64 >= M) return;
+  const uint32_t s = (uint32_t)s64, e = (uint32_t)min<uint64_t>(s64 + W, M);
+  const uint32_t cw = (uint32_t)(W / MSM_MERGE_FAN);
+  // the children's open slots of large buckets, in key order
+  uint32_t sb[2 * MSM_MERGE_FAN];
+  size_t si[2 * MSM_MERGE_FAN];
+  int ns = 0;
+#pragma unroll
+  for (int c = 0; c < MSM_MERGE_FAN; c++) {
+    const uint32_t cs = s + c * cw;
+    if (cs < e) {
+      const uint32_t ce = min(cs + cw, e);
+      const size_t v = (size_t)MSM_MERGE_FAN * u + c;
+      uint32_t b = key[cs];
+      if (off[b] < cs && big_bucket(off, b, K)) { sb[ns] = b; si[ns] = 2 * v; ns++; }
+      b = key[ce - 1];
+      if (off[b + 1] > ce && off[b] >= cs && big_bucket(off, b, K)) { sb[ns] = b; si[ns] = 2 * v + 1; ns++; }
+    }
+  }
+  int k = 0;
+  while (k < ns) {
+    const uint32_t b = sb[k];
+    X acc = ld_vec(&in[si[k]]);
+    for (k++; k < ns && sb[k] == b; k++) acc = xyzz_add(acc, ld_vec(&in[si[k]]));
+    if (off[b] >= s && off[b + 1] <= e) st_vec(&buckets[b], acc);   // complete
+    else if (off[b] < s) st_vec(&out[2 * (size_t)u], acc);           // open at the start
+    else st_vec(&out[2 * (size_t)u + 1], acc);                       // open at the end
   }
 }
 
-// One workgroup per row (C_hi, 2^kc contiguous buckets) or column
-// (D_lo, 2^kr buckets at stride 2^kc) of every window.  <= 256 buckets each.
+// ------------------------------------------------------------- reduce ---
+// One wave64 per sum: lane l folds terms l, l+64, ... serially (all lanes
+// busy), then a 6-step butterfly over __shfl_xor (no LDS, so occupancy is
+// set by VGPRs alone; a G2 point is 96 dwords -- 96 cross-lane moves per
+// step against ~20K instructions per add).  Both phases run through ONE
+// xyzz_add call site: the loop is not unrolled, so the kernel's code stays
+// a single add (I-cache) instead of 1 + 6 inlined copies.
+template <class X>
+__device__ __forceinline__ X shfl_xor_point(const X& v, int d) {
+  constexpr int NW = sizeof(X) / 4;
+  X o;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&v);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+  for (int k = 0; k < NW; k++) dst[k] = __shfl_xor(src[k], d);
+  return o;
+}
+
+constexpr int MSM_RED_WAVES = 4;   // sums per 256-thread workgroup
+
+// Row sums C_hi (2^kc contiguous buckets) and column sums D_lo (2^kr buckets
+// at stride 2^kc) of every window, one wave each.
 template <class C>
-__global__ void __launch_bounds__(256) k_msm_rowcol(MsmPlan p, const uint32_t* __restrict__ off,
-                                                    const typename C::X* __restrict__ buckets,
-                                                    typename C::X* __restrict__ rc) {
+__global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_rowcol(MsmPlan p, const uint32_t* __restrict__ off,
+                                                                  const typename C::X* __restrict__ buckets,
+                                                                  typename C::X* __restrict__ rc) {
   using X = typename C::X;
-  __shared__ X sh[256];
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = blockIdx.x * MSM_RED_WAVES + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  if (b >= p.nrc) return;   // whole waves
   int w = 0;
   while (b >= p.rcoff[w + 1]) w++;
   const uint32_t i = b - p.rcoff[w];
@@ -280,46 +365,63 @@ __global__ void __launch_bounds__(256) k_msm_rowcol(MsmPlan p, const uint32_t* _
   } else {
     len = rows; g0 = p.boff[w] + (i - rows); stride = cols;
   }
+  const uint32_t niter = (len + 63) >> 6;
   X v;
   xyzz_set_inf(v);
-  const uint32_t t = threadIdx.x;
-  if (t < len) {
-    const uint32_t g = g0 + t * stride;
-    if (off[g + 1] != off[g]) v = ld_vec(&buckets[g]);
+#pragma unroll 1
+  for (uint32_t it = 0; it < niter + 6; it++) {
+    X o;
+    if (it < niter) {
+      const uint32_t t = it * 64 + lane, g = g0 + t * stride;
+      if (t < len && off[g + 1] != off[g]) o = ld_vec(&buckets[g]);
+      else xyzz_set_inf(o);
+    } else {
+      o = shfl_xor_point(v, 1 << (it - niter));
+    }
+    v = xyzz_add(v, o);
   }
-  tree_sum(sh, v, len);
-  if (t == 0) st_vec(&rc[b], sh[0]);
+  if (lane == 0) st_vec(&rc[b], v);
 }
 
-// One workgroup per quantity: U^C_b (rows with bit b), U^D_b (columns with
-// bit b), P (all columns) of every window.
+// Quantities U^C_b (rows with bit b), U^D_b (columns with bit b) and P (all
+// columns) of every window, one wave each.
 template <class C>
-__global__ void __launch_bounds__(256) k_msm_quant(MsmPlan p, const typename C::X* __restrict__ rc,
-                                                   typename C::X* __restrict__ res) {
+__global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_quant(MsmPlan p, const typename C::X* __restrict__ rc,
+                                                                 typename C::X* __restrict__ res) {
   using X = typename C::X;
-  __shared__ X sh[256];
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = blockIdx.x * MSM_RED_WAVES + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  if (b >= p.nq) return;
   int w = 0;
   while (b >= p.qoff[w + 1]) w++;
   const uint32_t q = b - p.qoff[w];
   const uint32_t kr = p.kr[w], kc = p.kc[w];
   const uint32_t rows = 1u << kr, cols = 1u << kc;
-  const uint32_t t = threadIdx.x;
-  uint32_t len;
-  bool take;
+  uint32_t len, bit;
   const X* src;
   if (q < kr) {               // U^C_q
-    len = rows; src = rc + p.rcoff[w]; take = (t >> q) & 1;
+    len = rows; src = rc + p.rcoff[w]; bit = q;
   } else if (q < kr + kc) {   // U^D_{q-kr}
-    len = cols; src = rc + p.rcoff[w] + rows; take = (t >> (q - kr)) & 1;
+    len = cols; src = rc + p.rcoff[w] + rows; bit = q - kr;
   } else {                    // P
-    len = cols; src = rc + p.rcoff[w] + rows; take = true;
+    len = cols; src = rc + p.rcoff[w] + rows; bit = 32;
   }
+  const uint32_t niter = (len + 63) >> 6;
   X v;
   xyzz_set_inf(v);
-  if (t < len && take) v = ld_vec(&src[t]);
-  tree_sum(sh, v, len);
-  if (t == 0) st_vec(&res[b], sh[0]);
+#pragma unroll 1
+  for (uint32_t it = 0; it < niter + 6; it++) {
+    X o;
+    if (it < niter) {
+      const uint32_t t = it * 64 + lane;
+      if (t < len && (bit == 32 || ((t >> bit) & 1))) o = ld_vec(&src[t]);
+      else xyzz_set_inf(o);
+    } else {
+      o = shfl_xor_point(v, 1 << (it - niter));
+    }
+    v = xyzz_add(v, o);
+  }
+  if (lane == 0) st_vec(&res[b], v);
 }
 
 // ------------------------------------------------------------ driver -----
@@ -333,7 +435,10 @@ void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scal
   const size_t M = (size_t)n * p.nwin;
   if (M >= 0x80000000ull) throw Error(ZK_ERR_ARG, "msm: too many (point, window) entries");
   const uint32_t nblk = ceil_div(p.G, MSM_SCAN_BLOCK);
-  w.counts.ensure(sizeof(uint32_t) * (p.G + 1));
+  if (w.counts.bytes < sizeof(uint32_t) * (p.G + 1)) {   // zero once; k_scan_down re-zeroes
+    w.counts.ensure(sizeof(uint32_t) * (p.G + 1));
+    ZK_HIP(hipMemsetAsync(w.counts.p, 0, w.counts.bytes, st));
+  }
   w.off.ensure(sizeof(uint32_t) * (p.G + 1));
   w.cursor.ensure(sizeof(uint32_t) * (p.G + 1));
   w.scan_part.ensure(sizeof(uint32_t) * nblk);
@@ -342,12 +447,12 @@ void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scal
   w.buckets.ensure(sizeof(X) * p.G);
   const size_t nthr_max = (M + p.K - 1) / p.K + 1;
   w.partials.ensure(sizeof(X) * 2 * nthr_max);
+  w.partials2.ensure(sizeof(X) * (nthr_max + 2));
   w.rc.ensure(sizeof(X) * p.nrc);
   w.res.ensure(sizeof(X) * p.nq);
 
   Prof* pf = w.prof;
   const bool g2 = sizeof(typename C::A) == sizeof(G2A);
-  ZK_HIP(hipMemsetAsync(w.counts.p, 0, sizeof(uint32_t) * (p.G + 1), st));
   int ph = pf ? pf->begin(st, "msm_sort", n) : -1;   // digits + scan + scatter
   if (n) {
     const uint32_t nb = ceil_div(n, 256);
@@ -386,13 +491,29 @@ void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scal
     ZK_LAUNCH_CHECK();
     if (pf) pf->end(st, ph);
   }
-  ph = pf ? pf->begin(st, "msm_reduce", p.G) : -1;   // fixup + row/col + quantities
+  ph = pf ? pf->begin(st, "msm_merge", p.G) : -1;   // buckets split across chunks
   k_msm_fixup<C><<<ceil_div(p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), p.G, p.K, w.buckets.as<X>(),
                                                       w.partials.as<X>());
   ZK_LAUNCH_CHECK();
-  k_msm_rowcol<C><<<p.nrc, 256, 0, st>>>(p, w.off.as<uint32_t>(), w.buckets.as<X>(), w.rc.as<X>());
+  {
+    X* a = w.partials.as<X>();
+    X* b = w.partials2.as<X>();
+    const uint64_t fix_span = (uint64_t)p.K * MSM_FIX_MAX;   // smaller buckets never reach the merge
+    for (uint64_t W = (uint64_t)p.K * MSM_MERGE_FAN; W / MSM_MERGE_FAN < M; W *= MSM_MERGE_FAN) {
+      if (M <= fix_span) break;
+      const uint32_t groups = (uint32_t)((M + W - 1) / W);
+      k_msm_merge<C><<<ceil_div(groups, 128), 128, 0, st>>>(w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.K,
+                                                             W, w.buckets.as<X>(), a, b);
+      ZK_LAUNCH_CHECK();
+      std::swap(a, b);
+    }
+  }
+  if (pf) pf->end(st, ph);
+  ph = pf ? pf->begin(st, "msm_bucket_sum", p.G) : -1;   // row/col sums + quantities
+  k_msm_rowcol<C><<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.off.as<uint32_t>(),
+                                                                                w.buckets.as<X>(), w.rc.as<X>());
   ZK_LAUNCH_CHECK();
-  k_msm_quant<C><<<p.nq, 256, 0, st>>>(p, w.rc.as<X>(), w.res.as<X>());
+  k_msm_quant<C><<<ceil_div(p.nq, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.rc.as<X>(), w.res.as<X>());
   ZK_LAUNCH_CHECK();
   if (pf) pf->end(st, ph);
 }

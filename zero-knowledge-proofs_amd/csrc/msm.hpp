@@ -12,7 +12,8 @@
 //   3 scatter  (point index | sign) entries grouped by bucket (counting sort)
 //   4 accum    fixed K entries per thread, XYZZ += affine with run-length
 //              flush: load-balanced whatever the digit distribution
-//   5 fixup    buckets split across threads: sum the per-thread partials
+//   5 merge    buckets split across chunks: log-depth segmented merge of
+//              the per-chunk open pieces (k_msm_merge)
 //   6 rowcol   window w's nb = 2^(kr+kc) buckets seen as a 2^kr x 2^kc grid,
 //              bucket m = hi*2^kc + lo has weight m+1 = hi*2^kc + lo + 1, so
 //              sum_m (m+1) B_m = 2^kc sum_hi hi C_hi + sum_lo (lo+1) D_lo with
@@ -66,7 +67,7 @@ MsmPlan msm_make_plan(uint32_t n, int bits, int sw, int force_c = 0);
 
 // Device workspace of one in-flight MSM.
 struct MsmWork {
-  DevBuf counts, off, cursor, scan_part, ent, key, buckets, partials, rc, res;
+  DevBuf counts, off, cursor, scan_part, ent, key, buckets, partials, partials2, rc, res;
   PinnedBuf host_res;
   MsmPlan plan{};
   Prof* prof = nullptr;  // optional live kernel timing

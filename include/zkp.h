@@ -101,8 +101,9 @@ void zk_ctx_destroy(zk_ctx *ctx);
 const char *zk_last_error(const zk_ctx *ctx);
 int zk_ctx_synchronize(zk_ctx *ctx);
 /* Live kernel timing: HIP events recorded on the launching stream around
- * each kernel phase (msm_sort, msm_accum_g1, msm_accum_g2, msm_reduce, ntt,
- * quotient_eval, quotient_misc).  No reference counterpart (measurement). */
+ * each kernel phase (msm_sort, msm_accum_g1, msm_accum_g2, msm_merge,
+ * msm_bucket_sum, ntt, quotient_eval, quotient_misc).  No reference
+ * counterpart (measurement). */
 int zk_ctx_profile(zk_ctx *ctx, int enable);
 /* names: '\0'-separated phase names; per phase: total ms, launches, work
  * units (scalar-point pairs for msm_*, elements for ntt/quotient). */

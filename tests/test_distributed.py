@@ -1,0 +1,167 @@
+"""Multi-process path on CPU (gloo, world_size 2): the one exchange step of
+the sharded prover and the fold after it.
+
+On the GPU each rank runs zk_groth16_prove_partial over its contiguous
+slice of every base vector and the 1536-byte partials meet in ONE
+all-gather (RCCL in bench.py).  Here the per-rank partials are built by the
+oracle from a golden case split into two base ranges (exactly the linear
+decomposition the shards compute), exchanged with torch.distributed
+all_gather over gloo, and folded by zk_groth16_prove_combine (host code in
+libzkp_amd.so, no GPU needed).  The folded proof must equal the golden
+proof bit for bit.
+
+Partial layout (prove.hip `struct Partial`): host XYZZ points in Montgomery
+form with R = 2^384 -- A, B1, IC, H (G1: X, Y, ZZ, ZZZ, 6 limbs each), then
+B2 (G2: 12 limbs each), then an int32 status; zero-padded to 1536 bytes.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from helpers import fr_rows, g1_words, g2_words, golden, proof_words
+
+P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+RM = (1 << 384) % P
+MASK = (1 << 64) - 1
+PARTIAL_BYTES = 1536
+
+
+def _limbs(v, k):
+    return [(v >> (64 * i)) & MASK for i in range(k)]
+
+
+def _int(words):
+    return sum(int(w) << (64 * i) for i, w in enumerate(words))
+
+
+def _xyzz_g1(w):
+    """zk_g1_affine words -> host Montgomery XYZZ limbs (24 u64)."""
+    if int(w[12]) & 0xFF:
+        return [0] * 6 + _limbs(RM, 6) + [0] * 12
+    x, y = _int(w[0:6]), _int(w[6:12])
+    return _limbs(x * RM % P, 6) + _limbs(y * RM % P, 6) + _limbs(RM, 6) * 2
+
+
+def _xyzz_g2(w):
+    if int(w[24]) & 0xFF:
+        return [0] * 12 + _limbs(RM, 6) + [0] * 6 + [0] * 24
+    c = [_int(w[6 * i:6 * i + 6]) * RM % P for i in range(4)]
+    one = _limbs(RM, 6) + [0] * 6
+    return sum((_limbs(v, 6) for v in c), []) + one + one
+
+
+def _partial(A, B1, IC, H, B2):
+    words = _xyzz_g1(A) + _xyzz_g1(B1) + _xyzz_g1(IC) + _xyzz_g1(H) + _xyzz_g2(B2)
+    raw = np.array(words, dtype=np.uint64).tobytes() + np.int32(0).tobytes()
+    return raw + b"\0" * (PARTIAL_BYTES - len(raw))
+
+
+def shard_partials(oracle, case, world):
+    """Per-rank partials of `case`: rank k takes base range k of `world`
+    contiguous ranges; the fixed terms (alpha, beta, r delta, s delta) go to
+    rank 0, as zk_pk_upload_shard places them."""
+    pk = case["pk"]
+    g1 = lambda p: np.array(g1_words(p), dtype=np.uint64)
+    g2 = lambda p: np.array(g2_words(p), dtype=np.uint64)
+    z = [int(h, 16) for h in case["z"]]
+    w = [v & MASK for v in z]                                  # core:156-161
+    h = [int(x, 16) & MASK for x in case["h"]]                 # core:203-208
+    r, s = int(case["r"], 16), int(case["s"], 16)
+    l = case["num_public"]
+
+    def msm1(points, scal):
+        if not points:
+            return g1(None)
+        return oracle.msm_g1(np.array(points, dtype=np.uint64),
+                             fr_rows([f"{v:x}" for v in scal]))
+
+    def msm2(points, scal):
+        if not points:
+            return g2(None)
+        return oracle.msm_g2(np.array(points, dtype=np.uint64),
+                             fr_rows([f"{v:x}" for v in scal]))
+
+    def rng(length, k):
+        return length * k // world, length * (k + 1) // world
+
+    a = [g1(p) for p in pk["a_g1"]]
+    b1 = [g1(p) for p in pk["b_g1"]]
+    b2 = [g2(p) for p in pk["b_g2"]]
+    ic = [g1(p) for p in pk["ic_g1"]]
+    hg = [g1(p) for p in pk["h_g1"]]
+    wic = w[l + 1:]
+    nh = min(len(h), len(hg))                                  # core:211 zips
+    parts = []
+    for k in range(world):
+        lo, hi = rng(len(a), k)
+        pa, sa = a[lo:hi], w[lo:hi]
+        pb1, sb1 = b1[lo:hi], w[lo:hi]
+        lo2, hi2 = rng(len(b2), k)
+        pb2, sb2 = b2[lo2:hi2], w[lo2:hi2]
+        lo3, hi3 = rng(len(ic), k)
+        pic, sic = ic[lo3:hi3], wic[lo3:hi3]
+        lo4, hi4 = rng(nh, k)
+        ph, sh = hg[lo4:hi4], h[lo4:hi4]
+        if k == 0:
+            pa, sa = [g1(pk["alpha_g1"]), g1(pk["delta_g1"])] + pa, [1, r] + sa
+            pb1, sb1 = [g1(pk["beta_g1"])] + pb1, [1] + sb1
+            pb2, sb2 = [g2(pk["beta_g2"]), g2(pk["delta_g2"])] + pb2, [1, s] + sb2
+        parts.append(_partial(msm1(pa, sa), msm1(pb1, sb1), msm1(pic, sic), msm1(ph, sh), msm2(pb2, sb2)))
+    return parts
+
+
+def _free_port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _worker(rank, world, port, parts, r, s, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = torch.frombuffer(bytearray(parts[rank]), dtype=torch.uint8)
+        bufs = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(bufs, mine)                            # the one exchange
+        if rank == 0:
+            import importlib
+            zkp = importlib.import_module("zero-knowledge-proofs_amd")
+            proof = zkp.Prover.combine([b.numpy().tobytes() for b in bufs], r, s)
+            np.save(out_path, np.asarray(proof.words, dtype=np.uint64))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["synthetic_8", "random_5x9_pub2"])
+def test_gloo_allgather_combine(oracle, tmp_path, name):
+    case = next(c for c in golden()["prove"] if c["name"] == name)
+    world = 2
+    parts = shard_partials(oracle, case, world)
+    out = str(tmp_path / "proof.npy")
+    mp.spawn(_worker, args=(world, _free_port(), parts, int(case["r"], 16), int(case["s"], 16), out),
+             nprocs=world, join=True)
+    assert list(np.load(out)) == proof_words(case)
+
+
+def test_combine_single_partial_equals_golden(zkp, oracle):
+    """world 1: the same fold with one partial (what zk_groth16_prove does)."""
+    case = next(c for c in golden()["prove"] if c["name"] == "synthetic_4")
+    parts = shard_partials(oracle, case, 1)
+    proof = zkp.Prover.combine(parts, int(case["r"], 16), int(case["s"], 16))
+    assert list(proof.words) == proof_words(case)
+
+
+def test_combine_propagates_error_status(zkp, oracle):
+    case = next(c for c in golden()["prove"] if c["name"] == "synthetic_4")
+    parts = shard_partials(oracle, case, 2)
+    bad = bytearray(parts[1])
+    off = 4 * 24 * 8 + 4 * 12 * 8                             # status after A, B1, IC, H, B2
+    bad[off:off + 4] = np.int32(2).tobytes()                   # ZK_ERR_INVALID_WITNESS on rank 1
+    with pytest.raises(zkp.InvalidWitness):
+        zkp.Prover.combine([parts[0], bytes(bad)], 1, 1)

@@ -16,7 +16,7 @@ def test_ntt_golden(ctx, oracle, vec):
     assert oracle.fr_ints(ctx.ntt(x, coset=7)) == [int(a, 16) for a in vec["coset_fft_g7"]]
 
 
-@pytest.mark.parametrize("log_n", [1, 2, 3, 5, 9, 10, 11, 12, 13, 14, 16])
+@pytest.mark.parametrize("log_n", [1, 2, 3, 5, 9, 10, 11, 12, 13, 14, 16, 18, 20, 21, 22])
 def test_ntt_vs_oracle(ctx, oracle, log_n):
     x = oracle.random_fr(1 << log_n, 40 + log_n)
     assert np.array_equal(ctx.ntt(x), oracle.fft(x))

@@ -14,24 +14,31 @@
 
 #define ZK_DI __device__ __forceinline__
 
-// 16-byte vector global loads / stores of whole field elements / points
+// 16-byte vector global loads / stores of whole field elements / points.
+// __builtin_memcpy (not pointer punning into the destination) keeps arrays
+// of elements promotable to registers.
 template <class T>
 ZK_DI T ld_vec(const T* p) {
   static_assert(sizeof(T) % 16 == 0, "16-byte multiple");
   T r;
   const uint4* s = reinterpret_cast<const uint4*>(p);
-  uint4* d = reinterpret_cast<uint4*>(&r);
 #pragma unroll
-  for (int i = 0; i < (int)(sizeof(T) / 16); i++) d[i] = s[i];
+  for (int i = 0; i < (int)(sizeof(T) / 16); i++) {
+    const uint4 u = s[i];
+    __builtin_memcpy(reinterpret_cast<char*>(&r) + 16 * i, &u, 16);
+  }
   return r;
 }
 template <class T>
 ZK_DI void st_vec(T* p, const T& v) {
   static_assert(sizeof(T) % 16 == 0, "16-byte multiple");
-  const uint4* s = reinterpret_cast<const uint4*>(&v);
   uint4* d = reinterpret_cast<uint4*>(p);
 #pragma unroll
-  for (int i = 0; i < (int)(sizeof(T) / 16); i++) d[i] = s[i];
+  for (int i = 0; i < (int)(sizeof(T) / 16); i++) {
+    uint4 u;
+    __builtin_memcpy(&u, reinterpret_cast<const char*>(&v) + 16 * i, 16);
+    d[i] = u;
+  }
 }
 
 template <class P>

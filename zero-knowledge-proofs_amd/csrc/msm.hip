@@ -31,8 +31,7 @@ MsmPlan msm_make_plan(uint32_t n, int bits, int sw, int force_c) {
   if (const char* e = getenv("ZK_MSM_C")) best_c = std::max(4, std::min(16, atoi(e)));
   p.c = best_c;
   p.nwin = (bits + p.c - 1) / p.c;
-  p.K = 32;
-  if (const char* e = getenv("ZK_MSM_K")) p.K = std::max(1, atoi(e));
+
   uint32_t G = 0, rc = 0, q = 0;
   for (int w = 0; w < p.nwin; w++) {
     const int width = (w == p.nwin - 1) ? bits - p.c * w : p.c;
@@ -206,6 +205,12 @@ __device__ __forceinline__ typename C::A load_point(const typename C::A* __restr
   return a;
 }
 
+// Chunk length: the M non-zero digits (known on device only) split evenly
+// over the T accumulate threads, T = one full-occupancy wave set of the
+// chip, so every launch is exactly one balanced round whatever the digit
+// distribution.
+__device__ __forceinline__ uint32_t chunk_len(uint32_t M, uint32_t T) { return M ? (M + T - 1) / T : 1u; }
+
 // Thread t owns sorted entries [tK, tK+K).  One mixed add per entry (uniform
 // across the wave); at a bucket change the finished run is flushed:
 //   complete bucket                        -> buckets[g]
@@ -215,15 +220,16 @@ template <class C>
 __global__ void __launch_bounds__(128) k_msm_accum(const typename C::A* __restrict__ bases,
                                                    const uint32_t* __restrict__ ent,
                                                    const uint32_t* __restrict__ key,
-                                                   const uint32_t* __restrict__ off, uint32_t G, int K,
+                                                   const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
                                                    typename C::X* __restrict__ buckets,
                                                    typename C::X* __restrict__ partials) {
   using X = typename C::X;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t M = off[G];  // non-zero digits (known on device only)
-  const uint32_t start = t * (uint32_t)K;
-  if (start >= M) return;
-  const uint32_t end = min(start + (uint32_t)K, M);
+  const uint32_t K = chunk_len(M, T);
+  const uint32_t start = t * K;
+  if (t >= T || start >= M) return;
+  const uint32_t end = min(start + K, M);
   X acc;
   xyzz_set_inf(acc);
   uint32_t cur = key[start], run_start = start;
@@ -249,7 +255,7 @@ __global__ void __launch_bounds__(128) k_msm_accum(const typename C::A* __restri
 
 // Buckets whose entries span several accumulate chunks.  A bucket over
 // P = t1 - t0 + 1 chunks is tail(t0) + head(t0+1) + ... + head(t1):
-//  * P <= MSM_FIX_MAX (the common case: ~1-2): one thread sums the pieces
+//  * P <= fix_max (the common case: ~1-2): one thread sums the pieces
 //    serially (k_msm_fixup), all such buckets at once;
 //  * larger P (skewed scalars: a witness of mostly ones puts ~n entries in
 //    one bucket) goes through a log-depth segmented merge (k_msm_merge):
@@ -262,24 +268,24 @@ __global__ void __launch_bounds__(128) k_msm_accum(const typename C::A* __restri
 //    both decidable from the sorted keys and bucket offsets alone.  A level
 //    reads its children's <= 8 slots in key order, writes buckets that are
 //    now complete and passes the rest up: log4(M/K) levels of <= 7 adds.
-constexpr uint32_t MSM_FIX_MAX = 4;
 constexpr int MSM_MERGE_FAN = 4;
 
-__device__ __forceinline__ bool big_bucket(const uint32_t* off, uint32_t b, uint32_t K) {
-  return (off[b + 1] - 1) / K - off[b] / K + 1 > MSM_FIX_MAX;
+__device__ __forceinline__ bool big_bucket(const uint32_t* off, uint32_t b, uint32_t K, uint32_t fix_max) {
+  return (off[b + 1] - 1) / K - off[b] / K + 1 > fix_max;
 }
 
 template <class C>
-__global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ off, uint32_t G, uint32_t K,
+__global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ off, uint32_t G, uint32_t T, uint32_t fix_max,
                                                    typename C::X* __restrict__ buckets,
                                                    const typename C::X* __restrict__ partials) {
   using X = typename C::X;
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
+  const uint32_t K = chunk_len(off[G], T);
   const uint32_t bs = off[g], be = off[g + 1];
   if (be == bs) return;
   const uint32_t t0 = bs / K, t1 = (be - 1) / K;
-  if (t0 == t1 || t1 - t0 + 1 > MSM_FIX_MAX) return;
+  if (t0 == t1 || t1 - t0 + 1 > fix_max) return;
   X acc = ld_vec(&partials[2 * (size_t)t0 + 1]);
   for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, ld_vec(&partials[2 * (size_t)t]));
   st_vec(&buckets[g], acc);
@@ -287,13 +293,16 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
 
 template <class C>
 __global__ void __launch_bounds__(128) k_msm_merge(const uint32_t* __restrict__ key,
-                                                   const uint32_t* __restrict__ off, uint32_t G, uint32_t K,
-                                                   uint64_t W, typename C::X* __restrict__ buckets,
+                                                   const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
+                                                   uint32_t fix_max, uint32_t level,
+                                                   typename C::X* __restrict__ buckets,
                                                    const typename C::X* __restrict__ in,
                                                    typename C::X* __restrict__ out) {
   using X = typename C::X;
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t M = off[G];
+  const uint32_t K = chunk_len(M, T);
+  const uint64_t W = (uint64_t)K << (2 * level);   // MSM_MERGE_FAN = 4
   const uint64_t s64 = (uint64_t)u * W;
   if (s64 >= M) return;
   const uint32_t s = (uint32_t)s64, e = (uint32_t)min<uint64_t>(s64 + W, M);
@@ -309,9 +318,9 @@ __global__ void __launch_bounds__(128) k_msm_merge(const uint32_t* __restrict__ 
       const uint32_t ce = min(cs + cw, e);
       const size_t v = (size_t)MSM_MERGE_FAN * u + c;
       uint32_t b = key[cs];
-      if (off[b] < cs && big_bucket(off, b, K)) { sb[ns] = b; si[ns] = 2 * v; ns++; }
+      if (off[b] < cs && big_bucket(off, b, K, fix_max)) { sb[ns] = b; si[ns] = 2 * v; ns++; }
       b = key[ce - 1];
-      if (off[b + 1] > ce && off[b] >= cs && big_bucket(off, b, K)) { sb[ns] = b; si[ns] = 2 * v + 1; ns++; }
+      if (off[b + 1] > ce && off[b] >= cs && big_bucket(off, b, K, fix_max)) { sb[ns] = b; si[ns] = 2 * v + 1; ns++; }
     }
   }
   int k = 0;
@@ -425,6 +434,22 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_quant(MsmPlan p, con
 }
 
 // ------------------------------------------------------------ driver -----
+// Accumulate threads: one full-occupancy round of the chip (blocks per CU
+// from the occupancy calculator x CUs x 128), x ZK_MSM_ROUNDS for tuning.
+template <class C>
+static uint32_t accum_threads() {
+  static const uint32_t T = [] {
+    int dev = 0, cus = 0, per_cu = 0;
+    ZK_HIP(hipGetDevice(&dev));
+    ZK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_accum<C>, 128, 0));
+    int rounds = 1;
+    if (const char* e = getenv("ZK_MSM_ROUNDS")) rounds = std::max(1, atoi(e));
+    return (uint32_t)std::max(1, per_cu * cus * 128 * rounds);
+  }();
+  return T;
+}
+
 template <class C>
 void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scalars, int sw, uint32_t n,
                 int bits, hipStream_t st) {
@@ -445,9 +470,11 @@ void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scal
   w.ent.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
   w.key.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
   w.buckets.ensure(sizeof(X) * p.G);
-  const size_t nthr_max = (M + p.K - 1) / p.K + 1;
-  w.partials.ensure(sizeof(X) * 2 * nthr_max);
-  w.partials2.ensure(sizeof(X) * (nthr_max + 2));
+  p.T = accum_threads<C>();
+  p.fix_max = 8;
+  if (const char* e = getenv("ZK_MSM_FIX")) p.fix_max = (uint32_t)std::max(1, atoi(e));
+  w.partials.ensure(sizeof(X) * 2 * (size_t)p.T);
+  w.partials2.ensure(sizeof(X) * ((size_t)p.T / 2 + 2));
   w.rc.ensure(sizeof(X) * p.nrc);
   w.res.ensure(sizeof(X) * p.nq);
 
@@ -480,30 +507,28 @@ void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scal
     ZK_LAUNCH_CHECK();
   }
   if (pf) pf->end(st, ph);
-  // The number of non-zero digits M' <= M is only known on device: launch for
-  // M entries' worth of chunks; chunks beyond off[G] exit at once (no host sync).
+  // The number of non-zero digits M' <= M is known on device only: the T
+  // accumulate threads split it evenly there (chunk_len), no host sync.
   if (M) {
-    const uint32_t nthr = ceil_div(M, p.K);
     ph = pf ? pf->begin(st, g2 ? "msm_accum_g2" : "msm_accum_g1", n) : -1;
-    k_msm_accum<C><<<ceil_div(nthr, 128), 128, 0, st>>>(d_bases, w.ent.as<uint32_t>(), w.key.as<uint32_t>(),
-                                                         w.off.as<uint32_t>(), p.G, p.K, w.buckets.as<X>(),
-                                                         w.partials.as<X>());
+    k_msm_accum<C><<<ceil_div(p.T, 128), 128, 0, st>>>(d_bases, w.ent.as<uint32_t>(), w.key.as<uint32_t>(),
+                                                        w.off.as<uint32_t>(), p.G, p.T, w.buckets.as<X>(),
+                                                        w.partials.as<X>());
     ZK_LAUNCH_CHECK();
     if (pf) pf->end(st, ph);
   }
   ph = pf ? pf->begin(st, "msm_merge", p.G) : -1;   // buckets split across chunks
-  k_msm_fixup<C><<<ceil_div(p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), p.G, p.K, w.buckets.as<X>(),
+  k_msm_fixup<C><<<ceil_div(p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), p.G, p.T, p.fix_max, w.buckets.as<X>(),
                                                       w.partials.as<X>());
   ZK_LAUNCH_CHECK();
   {
     X* a = w.partials.as<X>();
     X* b = w.partials2.as<X>();
-    const uint64_t fix_span = (uint64_t)p.K * MSM_FIX_MAX;   // smaller buckets never reach the merge
-    for (uint64_t W = (uint64_t)p.K * MSM_MERGE_FAN; W / MSM_MERGE_FAN < M; W *= MSM_MERGE_FAN) {
-      if (M <= fix_span) break;
-      const uint32_t groups = (uint32_t)((M + W - 1) / W);
-      k_msm_merge<C><<<ceil_div(groups, 128), 128, 0, st>>>(w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.K,
-                                                             W, w.buckets.as<X>(), a, b);
+    // level l merges groups of 4^l chunks; T chunks at most
+    for (uint32_t level = 1; (1ull << (2 * (level - 1))) < p.T; level++) {
+      const uint32_t groups = (uint32_t)(((uint64_t)p.T + (1ull << (2 * level)) - 1) >> (2 * level));
+      k_msm_merge<C><<<ceil_div(groups, 128), 128, 0, st>>>(w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T,
+                                                             p.fix_max, level, w.buckets.as<X>(), a, b);
       ZK_LAUNCH_CHECK();
       std::swap(a, b);
     }

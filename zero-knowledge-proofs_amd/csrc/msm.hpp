@@ -10,8 +10,9 @@
 //   1 digits   signed c-bit window digits -> bucket histogram (global atomics)
 //   2 scan     3-phase parallel exclusive scan -> bucket offsets
 //   3 scatter  (point index | sign) entries grouped by bucket (counting sort)
-//   4 accum    fixed K entries per thread, XYZZ += affine with run-length
-//              flush: load-balanced whatever the digit distribution
+//   4 accum    the M non-zero digits split evenly over one full-occupancy
+//              round of threads, XYZZ += affine with run-length flush:
+//              load-balanced whatever the digit distribution
 //   5 merge    buckets split across chunks: log-depth segmented merge of
 //              the per-chunk open pieces (k_msm_merge)
 //   6 rowcol   window w's nb = 2^(kr+kc) buckets seen as a 2^kr x 2^kc grid,
@@ -52,7 +53,8 @@ constexpr int MSM_SCAN_BLOCK = 1024;  // elements per scan block (256 threads x 
 
 struct MsmPlan {
   int c, nwin, bits, sw;            // window bits, #windows, scalar bits, u64 words/scalar
-  int K;                            // accumulate chunk (entries per thread)
+  uint32_t T;                       // accumulate threads (chunk = ceil(M / T) on device)
+  uint32_t fix_max;                 // buckets over <= fix_max chunks: serial fixup, else merge
   uint32_t n;                       // points
   uint32_t G;                       // total buckets
   uint32_t nrc, nq;                 // total row/col sums, total quantities

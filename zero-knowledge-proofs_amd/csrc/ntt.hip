@@ -1,5 +1,6 @@
 // ntt.hip -- LDS-tiled radix-2 NTT passes over Fr (see ntt.hpp).
 #include <algorithm>
+#include <vector>
 
 #include "ntt.hpp"
 
@@ -7,98 +8,181 @@ namespace zk {
 
 constexpr int NTT_TILE_LOG = 11;  // 2048 elements x 32 B = 64 KiB of LDS per workgroup
 constexpr int NTT_THREADS = 256;
+constexpr int NTT_SM_LOG = 11;    // sub-transform twiddles: powers of omega_2048 (domain-independent)
+constexpr int NTT_TL_LOG = 12;    // omega_n^x = TL[x mod 4096] * TH[x / 4096]
 
 __device__ __forceinline__ uint32_t bitrev32(uint32_t x, uint32_t log_n) {
   return log_n ? (__builtin_bitreverse32(x) >> (32 - log_n)) : 0;
 }
 
-// One pass: stages s_lo .. s_lo+ns-1 on tiles of 2^ns rows x C columns.
-// Element (tile hi, row r, column lo) lives at i = hi*2^(s_lo+ns) + r*2^s_lo + lo.
-template <bool DIT>
-__global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(Fr* __restrict__ data, const Fr* __restrict__ tw,
-                                                          uint32_t log_n, uint32_t s_lo, uint32_t ns,
-                                                          uint32_t logC) {
-  extern __shared__ Fr sh[];
+struct NttTabs {
+  const Fr* sm;   // omega_2048^j, j < 1024 (or the inverse root)
+  const Fr* tl;   // omega_n^x, x < min(n, 4096)
+  const Fr* th;   // omega_n^(4096 y), y < n / 4096
+};
+
+// omega_n^x, x < n
+__device__ __forceinline__ Fr tw_full(const NttTabs& t, uint32_t x, uint32_t log_n) {
+  Fr w = ld_vec(&t.tl[x & ((1u << NTT_TL_LOG) - 1)]);
+  if (log_n > NTT_TL_LOG) w = fp_mul(w, ld_vec(&t.th[x >> NTT_TL_LOG]));
+  return w;
+}
+
+// One radix-2^R round of a tile's sub-transform: local stages
+// [lsb, lsb + R).  Each thread owns whole groups of 2^R elements (rows
+// r0 + m 2^lsb, one column), keeps them in registers for all R stages and
+// touches LDS once per round (16-byte accesses), so an 11-stage tile costs 4
+// LDS round trips and 4 barriers instead of 11.  Twiddle of local stage t
+// for row r: omega_(2^(t+1))^(r mod 2^t) = omega_2048^((r mod 2^t) 2^(10-t)).
+template <int R, int Q, bool DIT>
+__device__ __forceinline__ void ntt_stage(Fr (&x)[1 << R], const Fr* __restrict__ sm, uint32_t rlow, uint32_t lsb) {
+  constexpr int G = 1 << R;
+  const uint32_t t = lsb + Q;
+  Fr w[1 << Q];
+#pragma unroll
+  for (int k = 0; k < (1 << Q); k++) w[k] = ld_vec(&sm[(rlow + ((uint32_t)k << lsb)) << (NTT_SM_LOG - 1 - t)]);
+#pragma unroll
+  for (int i = 0; i < G / 2; i++) {
+    const int m = ((i >> Q) << (Q + 1)) | (i & ((1 << Q) - 1));
+    Fr u = x[m], v = x[m + (1 << Q)];
+    if (DIT) {
+      v = fp_mul(v, w[m & ((1 << Q) - 1)]);
+      x[m] = fp_add(u, v);
+      x[m + (1 << Q)] = fp_sub(u, v);
+    } else {
+      x[m] = fp_add(u, v);
+      x[m + (1 << Q)] = fp_mul(fp_sub(u, v), w[m & ((1 << Q) - 1)]);
+    }
+  }
+}
+
+template <int R, bool DIT>
+__device__ __forceinline__ void ntt_round(Fr* sh, const Fr* __restrict__ sm, uint32_t ns, uint32_t logC,
+                                          uint32_t lsb) {
+  constexpr int G = 1 << R;
   const uint32_t C = 1u << logC;
-  const uint32_t rows = 1u << ns;
-  const uint32_t tile_elems = rows << logC;
+  const uint32_t ngroups = (1u << (ns + logC)) >> R;
+  for (uint32_t g = threadIdx.x; g < ngroups; g += NTT_THREADS) {
+    const uint32_t c = g & (C - 1), rg = g >> logC;
+    const uint32_t rlow = rg & ((1u << lsb) - 1);
+    const uint32_t r0 = ((rg >> lsb) << (lsb + R)) | rlow;
+    Fr x[G];
+#pragma unroll
+    for (int m = 0; m < G; m++) x[m] = ld_vec(&sh[((r0 + ((uint32_t)m << lsb)) << logC) | c]);
+    if (DIT) {
+      ntt_stage<R, 0, DIT>(x, sm, rlow, lsb);
+      if constexpr (R > 1) ntt_stage<R, (R > 1 ? 1 : 0), DIT>(x, sm, rlow, lsb);
+      if constexpr (R > 2) ntt_stage<R, (R > 2 ? 2 : 0), DIT>(x, sm, rlow, lsb);
+    } else {
+      if constexpr (R > 2) ntt_stage<R, (R > 2 ? 2 : 0), DIT>(x, sm, rlow, lsb);
+      if constexpr (R > 1) ntt_stage<R, (R > 1 ? 1 : 0), DIT>(x, sm, rlow, lsb);
+      ntt_stage<R, 0, DIT>(x, sm, rlow, lsb);
+    }
+#pragma unroll
+    for (int m = 0; m < G; m++) st_vec(&sh[((r0 + ((uint32_t)m << lsb)) << logC) | c], x[m]);
+  }
+}
+
+// One pass = one four-step level.  The block of N = 2^(s_lo+ns) elements
+// at hi is a 2^ns x 2^s_lo matrix (row r, column lo); the pass runs the
+// 2^ns-point sub-transform down every column of its tile (C columns), whose
+// twiddles are powers of omega_(2^ns) only, and the inter-level twiddle
+// omega_N^(lo * bitrev(r)) is applied to the whole tile once: after the
+// columns for DIF (natural -> bit-reversed), before them for DIT (the
+// transpose).  With n = n1 n2, X[k1 + n1 k2] = sum_b w_n2^(b k2) w_n^(b k1)
+// sum_a x[a n2 + b] w_n1^(a k1); sub-transforms in place leave element k at
+// bitrev(k1) n2 + bitrev(k2) = bitrev_(log n)(k): exactly radix-2 DIF order.
+template <bool DIT>
+__global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(Fr* __restrict__ data, NttTabs tabs, uint32_t log_n,
+                                                          uint32_t s_lo, uint32_t ns, uint32_t logC) {
+  extern __shared__ uint4 sh_raw[];
+  Fr* sh = reinterpret_cast<Fr*>(sh_raw);
+  const uint32_t C = 1u << logC;
+  const uint32_t tile_elems = (1u << ns) << logC;
   const uint32_t lo_blocks = (1u << s_lo) >> logC;      // column blocks per hi
   const uint32_t tile = blockIdx.x;
   const uint32_t hi = tile / lo_blocks;
   const uint32_t lo0 = (tile % lo_blocks) << logC;
   const size_t base = ((size_t)hi << (s_lo + ns)) + lo0;
+  const uint32_t tw_shift = log_n - s_lo - ns;          // omega_N = omega_n^(2^tw_shift)
 
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) {
     const uint32_t r = k >> logC, c = k & (C - 1);
-    sh[k] = ld_vec(&data[base + ((size_t)r << s_lo) + c]);
+    Fr v = ld_vec(&data[base + ((size_t)r << s_lo) + c]);
+    if (DIT && s_lo) v = fp_mul(v, tw_full(tabs, ((lo0 + c) * bitrev32(r, ns)) << tw_shift, log_n));
+    st_vec(&sh[k], v);
   }
   __syncthreads();
-
-  const uint32_t nbf = tile_elems >> 1;
-  for (uint32_t st = 0; st < ns; st++) {
-    const uint32_t ls = DIT ? st : ns - 1 - st;    // local stage
-    const uint32_t s = s_lo + ls;                   // global stage: pairs (i, i + 2^s)
-    const uint32_t tw_shift = log_n - 1 - s;
-    for (uint32_t b = threadIdx.x; b < nbf; b += NTT_THREADS) {
-      const uint32_t c = b & (C - 1), rb = b >> logC;
-      const uint32_t r = ((rb >> ls) << (ls + 1)) | (rb & ((1u << ls) - 1));
-      const uint32_t k0 = (r << logC) | c, k1 = k0 + (1u << (ls + logC));
-      // exponent: (i mod 2^s) * n / 2^(s+1)
-      const uint32_t im = ((r & ((1u << ls) - 1)) << s_lo) | (lo0 + c);
-      const Fr w = ld_vec(&tw[(size_t)im << tw_shift]);
-      Fr u = sh[k0], v = sh[k1];
-      if (DIT) {
-        v = fp_mul(v, w);
-        sh[k0] = fp_add(u, v);
-        sh[k1] = fp_sub(u, v);
-      } else {
-        sh[k0] = fp_add(u, v);
-        sh[k1] = fp_mul(fp_sub(u, v), w);
-      }
+  // rounds of 3 stages (2 or 1 for the remainder): DIF top-down, DIT bottom-up
+  const uint32_t full = ns / 3, rem = ns % 3;
+  if (DIT) {
+    uint32_t lsb = 0;
+    for (uint32_t i = 0; i < full; i++, lsb += 3) {
+      ntt_round<3, true>(sh, tabs.sm, ns, logC, lsb);
+      __syncthreads();
     }
-    __syncthreads();
+    if (rem == 2) ntt_round<2, true>(sh, tabs.sm, ns, logC, lsb);
+    if (rem == 1) ntt_round<1, true>(sh, tabs.sm, ns, logC, lsb);
+  } else {
+    uint32_t lsb = ns;
+    for (uint32_t i = 0; i < full; i++) {
+      lsb -= 3;
+      ntt_round<3, false>(sh, tabs.sm, ns, logC, lsb);
+      __syncthreads();
+    }
+    if (rem == 2) ntt_round<2, false>(sh, tabs.sm, ns, logC, 0);
+    if (rem == 1) ntt_round<1, false>(sh, tabs.sm, ns, logC, 0);
   }
+  __syncthreads();
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) {
     const uint32_t r = k >> logC, c = k & (C - 1);
-    st_vec(&data[base + ((size_t)r << s_lo) + c], sh[k]);
+    Fr v = ld_vec(&sh[k]);
+    if (!DIT && s_lo) v = fp_mul(v, tw_full(tabs, ((lo0 + c) * bitrev32(r, ns)) << tw_shift, log_n));
+    st_vec(&data[base + ((size_t)r << s_lo) + c], v);
   }
 }
 
-static void run_pass(bool dit, Fr* d, const Fr* tw, uint32_t log_n, uint32_t s_lo, uint32_t ns,
+static void run_pass(bool dit, Fr* d, const NttTabs& t, uint32_t log_n, uint32_t s_lo, uint32_t ns,
                      hipStream_t st) {
-  const uint32_t logC = std::min<uint32_t>(s_lo, std::min<uint32_t>(2, NTT_TILE_LOG - ns));
+  const uint32_t logC = std::min<uint32_t>(s_lo, NTT_TILE_LOG - ns);
   const uint32_t tiles = (uint32_t)((1ull << log_n) >> (ns + logC));
   const size_t lds = sizeof(Fr) << (ns + logC);
   if (dit)
-    k_ntt_pass<true><<<tiles, NTT_THREADS, lds, st>>>(d, tw, log_n, s_lo, ns, logC);
+    k_ntt_pass<true><<<tiles, NTT_THREADS, lds, st>>>(d, t, log_n, s_lo, ns, logC);
   else
-    k_ntt_pass<false><<<tiles, NTT_THREADS, lds, st>>>(d, tw, log_n, s_lo, ns, logC);
+    k_ntt_pass<false><<<tiles, NTT_THREADS, lds, st>>>(d, t, log_n, s_lo, ns, logC);
   ZK_LAUNCH_CHECK();
 }
 
-// Stage grouping: up to 9 stages per pass while columns can be batched 4-wide
-// (coalesced 128 B rows), up to 11 in the final stride-1 pass.
-static uint32_t pass_stages(uint32_t s_lo, uint32_t remaining) {
-  uint32_t cap = s_lo >= 2 ? NTT_TILE_LOG - 2 : NTT_TILE_LOG - s_lo;
-  return std::min(cap, remaining);
+// Pass plan, top (first DIF pass) to bottom: the contiguous pass (s_lo = 0)
+// takes up to 11 stages; the rest are split evenly into strided passes of
+// <= 9 stages, so tiles keep >= 4 consecutive columns (128-byte rows).
+static std::vector<uint32_t> pass_plan(uint32_t L) {
+  const uint32_t last = std::min<uint32_t>(L, NTT_TILE_LOG);
+  const uint32_t rest = L - last;
+  std::vector<uint32_t> ns;
+  if (rest) {
+    const uint32_t np = (rest + (NTT_TILE_LOG - 2) - 1) / (NTT_TILE_LOG - 2);
+    for (uint32_t i = 0; i < np; i++) ns.push_back(rest / np + (i < rest % np ? 1 : 0));
+  }
+  ns.push_back(last);
+  return ns;
+}
+
+static NttTabs tabs_of(const NttDomain& dom, bool inv) {
+  return inv ? NttTabs{dom.ism.as<Fr>(), dom.itl.as<Fr>(), dom.ith.as<Fr>()}
+             : NttTabs{dom.sm.as<Fr>(), dom.tl.as<Fr>(), dom.th.as<Fr>()};
 }
 
 void ntt_dif(Fr* d, const NttDomain& dom, bool inv, hipStream_t st, Prof* pf) {
   const uint32_t L = dom.log_n;
   if (L == 0) return;
   const int ph = pf ? pf->begin(st, "ntt", (uint64_t)1 << L) : -1;
-  const Fr* tw = (inv ? dom.itw : dom.tw).as<Fr>();
-  // stages L-1 .. 0, top-down: choose pass sizes so that the last pass (s_lo = 0) is widest
-  uint32_t s_hi = L;  // exclusive
-  while (s_hi > 0) {
-    uint32_t ns = std::min<uint32_t>(s_hi, NTT_TILE_LOG);
-    uint32_t s_lo = s_hi - ns;
-    if (s_lo > 0) {               // a strided pass: at most 9 stages, and leave >= 0
-      ns = std::min<uint32_t>(ns, NTT_TILE_LOG - 2);
-      s_lo = s_hi - ns;
-    }
-    run_pass(false, d, tw, L, s_lo, ns, st);
-    s_hi = s_lo;
+  const NttTabs t = tabs_of(dom, inv);
+  uint32_t s_hi = L;
+  for (uint32_t ns : pass_plan(L)) {
+    run_pass(false, d, t, L, s_hi - ns, ns, st);
+    s_hi -= ns;
   }
   if (pf) pf->end(st, ph);
 }
@@ -107,12 +191,12 @@ void ntt_dit(Fr* d, const NttDomain& dom, bool inv, hipStream_t st, Prof* pf) {
   const uint32_t L = dom.log_n;
   if (L == 0) return;
   const int ph = pf ? pf->begin(st, "ntt", (uint64_t)1 << L) : -1;
-  const Fr* tw = (inv ? dom.itw : dom.tw).as<Fr>();
+  const NttTabs t = tabs_of(dom, inv);
+  const std::vector<uint32_t> plan = pass_plan(L);
   uint32_t s_lo = 0;
-  while (s_lo < L) {
-    uint32_t ns = pass_stages(s_lo, L - s_lo);
-    run_pass(true, d, tw, L, s_lo, ns, st);
-    s_lo += ns;
+  for (auto it = plan.rbegin(); it != plan.rend(); ++it) {
+    run_pass(true, d, t, L, s_lo, *it, st);
+    s_lo += *it;
   }
   if (pf) pf->end(st, ph);
 }
@@ -178,15 +262,27 @@ __global__ void k_coset_zinv(Fr* out, uint32_t log_n) {
 void ntt_domain_init(NttDomain& d, uint32_t log_n, hipStream_t st) {
   d.log_n = log_n;
   const size_t n = (size_t)1 << log_n;
-  const size_t half = std::max<size_t>(n / 2, 1);
-  d.tw.ensure(sizeof(Fr) * half);
-  d.itw.ensure(sizeof(Fr) * half);
+  const size_t nsm = (size_t)1 << (NTT_SM_LOG - 1);
+  const size_t ntl = std::min<size_t>(n, (size_t)1 << NTT_TL_LOG);
+  const size_t nth = std::max<size_t>(n >> NTT_TL_LOG, 1);
+  d.sm.ensure(sizeof(Fr) * nsm);
+  d.ism.ensure(sizeof(Fr) * nsm);
+  d.tl.ensure(sizeof(Fr) * ntl);
+  d.itl.ensure(sizeof(Fr) * ntl);
+  d.th.ensure(sizeof(Fr) * nth);
+  d.ith.ensure(sizeof(Fr) * nth);
   d.gpow.ensure(sizeof(Fr) * n);
   d.gipow.ensure(sizeof(Fr) * n);
   Fr one = fr_const(FrParams::ONE);
   Fr ninv = fr_const(FR_INV_2K[log_n]);
-  fr_powers(d.tw.as<Fr>(), fr_const(FR_ROOTS[log_n]), one, half, st);
-  fr_powers(d.itw.as<Fr>(), fr_const(FR_ROOTS_INV[log_n]), one, half, st);
+  fr_powers(d.sm.as<Fr>(), fr_const(FR_ROOTS[NTT_SM_LOG]), one, nsm, st);
+  fr_powers(d.ism.as<Fr>(), fr_const(FR_ROOTS_INV[NTT_SM_LOG]), one, nsm, st);
+  fr_powers(d.tl.as<Fr>(), fr_const(FR_ROOTS[log_n]), one, ntl, st);
+  fr_powers(d.itl.as<Fr>(), fr_const(FR_ROOTS_INV[log_n]), one, ntl, st);
+  if (log_n > NTT_TL_LOG) {   // omega_n^4096 = omega_(n / 4096)
+    fr_powers(d.th.as<Fr>(), fr_const(FR_ROOTS[log_n - NTT_TL_LOG]), one, nth, st);
+    fr_powers(d.ith.as<Fr>(), fr_const(FR_ROOTS_INV[log_n - NTT_TL_LOG]), one, nth, st);
+  }
   fr_powers(d.gpow.as<Fr>(), fr_const(FR_GEN), ninv, n, st);
   fr_powers(d.gipow.as<Fr>(), fr_const(FR_GEN_INV), ninv, n, st);
   d.zinv.ensure(sizeof(Fr));

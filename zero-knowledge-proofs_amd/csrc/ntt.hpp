@@ -7,10 +7,12 @@
 // omega_n = (7^((r-1)/2^32))^(2^(32 - log n)).
 //
 // Layout: Fr elements are 32 B (8 x u32 Montgomery limbs), contiguous.
-// A pass loads a tile of 2^ns rows x C consecutive columns into LDS
-// (<= 2048 elements = 64 KiB), runs ns radix-2 stages with workgroup
-// barriers, and writes it back: log n stages cost ceil(log n / ~9) HBM
-// round trips instead of log n.  DIF passes take natural order to
+// Four-step (recursive) structure: a pass loads a tile of 2^ns rows x C
+// consecutive columns into LDS (<= 2048 elements = 64 KiB), runs the
+// 2^ns-point sub-transform down its columns with twiddles from a small
+// cached table, and applies the inter-level twiddles once per element, so
+// log n stages cost ~log n / 10 HBM round trips and no per-butterfly
+// gathers from an n/2-entry table.  DIF passes take natural order to
 // bit-reversed order, DIT passes the reverse, so the quotient pipeline
 // (iNTT -> coset NTT -> divide -> coset iNTT) never needs a standalone
 // permutation except once, fused into its final gather.
@@ -23,8 +25,9 @@ namespace zk {
 // Per-domain constant tables, built on device once and cached by the ctx.
 struct NttDomain {
   uint32_t log_n = 0;
-  DevBuf tw;      // omega^k, k < n/2
-  DevBuf itw;     // omega^-k, k < n/2
+  DevBuf sm, ism;   // omega_2048^j, j < 1024 (and inverse): sub-transform twiddles
+  DevBuf tl, itl;   // omega_n^x, x < min(n, 4096)
+  DevBuf th, ith;   // omega_n^(4096 y), y < n / 4096
   DevBuf gpow;    // n^-1 * g^i, i < n   (coset shift g = 7)
   DevBuf gipow;   // n^-1 * g^-i, i < n
   DevBuf zinv;    // (g^n - 1)^-1: 1/Z on the coset g<w>

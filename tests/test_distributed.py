@@ -11,8 +11,9 @@ libzkp_amd.so, no GPU needed).  The folded proof must equal the golden
 proof bit for bit.
 
 Partial layout (prove.hip `struct Partial`): host XYZZ points in Montgomery
-form with R = 2^384 -- A, B1, IC, H (G1: X, Y, ZZ, ZZZ, 6 limbs each), then
-B2 (G2: 12 limbs each), then an int32 status; zero-padded to 1536 bytes.
+form with R = 2^384 -- A, B1, IC, H, SC = s A + r B1 (G1: X, Y, ZZ, ZZZ, 6
+limbs each), then B2 (G2: 12 limbs each), then an int32 status;
+zero-padded to 1536 bytes.
 """
 import os
 import socket
@@ -55,8 +56,8 @@ def _xyzz_g2(w):
     return sum((_limbs(v, 6) for v in c), []) + one + one
 
 
-def _partial(A, B1, IC, H, B2):
-    words = _xyzz_g1(A) + _xyzz_g1(B1) + _xyzz_g1(IC) + _xyzz_g1(H) + _xyzz_g2(B2)
+def _partial(A, B1, IC, H, SC, B2):
+    words = _xyzz_g1(A) + _xyzz_g1(B1) + _xyzz_g1(IC) + _xyzz_g1(H) + _xyzz_g1(SC) + _xyzz_g2(B2)
     raw = np.array(words, dtype=np.uint64).tobytes() + np.int32(0).tobytes()
     return raw + b"\0" * (PARTIAL_BYTES - len(raw))
 
@@ -111,7 +112,9 @@ def shard_partials(oracle, case, world):
             pa, sa = [g1(pk["alpha_g1"]), g1(pk["delta_g1"])] + pa, [1, r] + sa
             pb1, sb1 = [g1(pk["beta_g1"])] + pb1, [1] + sb1
             pb2, sb2 = [g2(pk["beta_g2"]), g2(pk["delta_g2"])] + pb2, [1, s] + sb2
-        parts.append(_partial(msm1(pa, sa), msm1(pb1, sb1), msm1(pic, sic), msm1(ph, sh), msm2(pb2, sb2)))
+        A, B1 = msm1(pa, sa), msm1(pb1, sb1)
+        SC = oracle.g1_add(oracle.g1_mul(A, s), oracle.g1_mul(B1, r))
+        parts.append(_partial(A, B1, msm1(pic, sic), msm1(ph, sh), SC, msm2(pb2, sb2)))
     return parts
 
 
@@ -161,7 +164,7 @@ def test_combine_propagates_error_status(zkp, oracle):
     case = next(c for c in golden()["prove"] if c["name"] == "synthetic_4")
     parts = shard_partials(oracle, case, 2)
     bad = bytearray(parts[1])
-    off = 4 * 24 * 8 + 4 * 12 * 8                             # status after A, B1, IC, H, B2
+    off = 5 * 24 * 8 + 4 * 12 * 8                             # status after A, B1, IC, H, SC, B2
     bad[off:off + 4] = np.int32(2).tobytes()                   # ZK_ERR_INVALID_WITNESS on rank 1
     with pytest.raises(zkp.InvalidWitness):
         zkp.Prover.combine([parts[0], bytes(bad)], 1, 1)

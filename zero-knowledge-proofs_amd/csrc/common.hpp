@@ -125,6 +125,13 @@ struct Prof {
     if (i < 0) return;
     ZK_HIP(hipEventRecord(pending[i].b, st));
   }
+  // host-side wall time of a phase (measured by the caller)
+  void add_host(const char* phase, double ms) {
+    if (!on) return;
+    PhaseStat& s = stats[phase];
+    s.ms += ms;
+    s.launches += 1;
+  }
   // after the stream has been synchronised
   void collect() {
     for (Rec& r : pending) {

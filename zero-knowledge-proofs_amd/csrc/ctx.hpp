@@ -29,11 +29,13 @@ struct zk_ctx {
   hipStream_t stream = nullptr;                 // main stream
   hipStream_t side[zk::NUM_SIDE] = {};          // G2 / IC / A+B1 MSM streams
   hipEvent_t ev_quot = nullptr, ev_scal = nullptr;
+  hipEvent_t ev_done[zk::NUM_MSM] = {};         // per-MSM completion (results downloaded)
   std::string err;
   zk::MsmWork msm[zk::NUM_MSM];
   std::map<uint32_t, std::unique_ptr<zk::NttDomain>> domains;
   // prove scratch
   zk::DevBuf z_canon, z_mont, qa, qb, qc, flags;
+  zk::PinnedBuf flags_host;
   zk::DevBuf scal[zk::NUM_MSM];
   zk::DevBuf tmp_bases, tmp_scal, tmp_fr;
   zk::Prof prof;

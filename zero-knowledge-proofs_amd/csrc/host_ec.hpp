@@ -249,6 +249,28 @@ inline X<F> mul_scalar(const X<F>& p, const uint64_t k[4]) {
   }
   return acc;
 }
+// k1*p + k2*q (Straus / Shamir, 4-bit windows): 256 doublings shared by both
+// scalars and <= 2 additions per window -- the s*pi_A + r*B_1 term of pi_C.
+template <class F>
+inline X<F> mul2_scalar(const X<F>& p, const uint64_t k1[4], const X<F>& q, const uint64_t k2[4]) {
+  X<F> tp[16], tq[16];
+  tp[0] = inf<F>();
+  tq[0] = inf<F>();
+  for (int i = 1; i < 16; i++) {
+    tp[i] = addp(tp[i - 1], p);
+    tq[i] = addp(tq[i - 1], q);
+  }
+  X<F> acc = inf<F>();
+  for (int w = 63; w >= 0; w--) {
+    for (int d = 0; d < 4; d++) acc = dbl(acc);
+    const int sh = (w & 15) * 4;
+    const unsigned d1 = (unsigned)(k1[w >> 4] >> sh) & 15u, d2 = (unsigned)(k2[w >> 4] >> sh) & 15u;
+    if (d1) acc = addp(acc, tp[d1]);
+    if (d2) acc = addp(acc, tq[d2]);
+  }
+  return acc;
+}
+
 // affine (Montgomery) from XYZZ: x = X/ZZ, y = Y/ZZZ.  Returns false at infinity.
 template <class F>
 inline bool to_affine(const X<F>& p, F& x, F& y) {

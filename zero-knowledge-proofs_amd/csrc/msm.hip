@@ -128,6 +128,49 @@ __global__ void __launch_bounds__(256) k_msm_digits(const uint64_t* __restrict__
   }
 }
 
+// Radix-sort path: one (bucket, entry) pair per (point, window), written
+// window-major (coalesced); a zero digit gets the key G, which sorts after
+// every bucket, so off[G] still counts the non-zero digits.
+template <int SW>
+__global__ void __launch_bounds__(256) k_msm_keys(const uint64_t* __restrict__ sc, MsmPlan p,
+                                                  uint32_t* __restrict__ key, uint32_t* __restrict__ ent) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  uint64_t s[SW];
+#pragma unroll
+  for (int k = 0; k < SW; k++) s[k] = sc[(size_t)i * SW + k];
+  uint32_t carry = 0;
+  const uint32_t half = 1u << (p.c - 1);
+  for (int w = 0; w < p.nwin; w++) {
+    const bool top = (w == p.nwin - 1);
+    const int width = top ? p.bits - p.c * w : p.c;
+    const uint32_t v = scal_window<SW>(s, p.c * w, width) + carry;
+    uint32_t mag;
+    bool neg = false;
+    if (!top && v > half) {
+      mag = (1u << p.c) - v;
+      neg = true;
+      carry = 1;
+    } else {
+      mag = v;
+      carry = 0;
+    }
+    const size_t o = (size_t)w * p.n + i;
+    key[o] = mag ? p.boff[w] + mag - 1 : p.G;
+    ent[o] = i | (neg ? 0x80000000u : 0u);
+  }
+}
+
+// off[g] = first sorted position with key >= g, for g in [0, G].
+__global__ void __launch_bounds__(256) k_msm_offsets(const uint32_t* __restrict__ key, uint32_t M, uint32_t G,
+                                                     uint32_t* __restrict__ off) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > M) return;
+  const uint32_t lo = i ? min(key[i - 1], G) + 1 : 0;     // keys in (key[i-1], key[i]] start at i
+  const uint32_t hi = i < M ? min(key[i], G) : G;
+  for (uint32_t g = lo; g <= hi; g++) off[g] = i;
+}
+
 // --------------------------------------------------------------- scan ---
 // 3-phase exclusive scan of G bucket counts: per-block sums, one scan of
 // the block sums, per-block scan with its base.  Writes off[0..G] and a
@@ -434,6 +477,18 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_quant(MsmPlan p, con
 }
 
 // ------------------------------------------------------------ driver -----
+void sort_pairs_u32(void* tmp, size_t& tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                    const uint32_t* vals_in, uint32_t* vals_out, size_t n, unsigned end_bit, hipStream_t st);
+
+// 0: rocPRIM radix sort (default), 1: atomic counting sort (ZK_MSM_SORT=count)
+static int msm_sort_mode() {
+  static const int mode = [] {
+    const char* e = getenv("ZK_MSM_SORT");
+    return (e && std::strcmp(e, "count") == 0) ? 1 : 0;
+  }();
+  return mode;
+}
+
 // Accumulate threads: one full-occupancy round of the chip (blocks per CU
 // from the occupancy calculator x CUs x 128), x ZK_MSM_ROUNDS for tuning.
 template <class C>
@@ -460,13 +515,7 @@ void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scal
   const size_t M = (size_t)n * p.nwin;
   if (M >= 0x80000000ull) throw Error(ZK_ERR_ARG, "msm: too many (point, window) entries");
   const uint32_t nblk = ceil_div(p.G, MSM_SCAN_BLOCK);
-  if (w.counts.bytes < sizeof(uint32_t) * (p.G + 1)) {   // zero once; k_scan_down re-zeroes
-    w.counts.ensure(sizeof(uint32_t) * (p.G + 1));
-    ZK_HIP(hipMemsetAsync(w.counts.p, 0, w.counts.bytes, st));
-  }
   w.off.ensure(sizeof(uint32_t) * (p.G + 1));
-  w.cursor.ensure(sizeof(uint32_t) * (p.G + 1));
-  w.scan_part.ensure(sizeof(uint32_t) * nblk);
   w.ent.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
   w.key.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
   w.buckets.ensure(sizeof(X) * p.G);
@@ -480,31 +529,61 @@ void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scal
 
   Prof* pf = w.prof;
   const bool g2 = sizeof(typename C::A) == sizeof(G2A);
-  int ph = pf ? pf->begin(st, "msm_sort", n) : -1;   // digits + scan + scatter
-  if (n) {
-    const uint32_t nb = ceil_div(n, 256);
-    if (sw == 1)
-      k_msm_digits<1, false><<<nb, 256, 0, st>>>(d_scalars, p, w.counts.as<uint32_t>(), nullptr, nullptr, nullptr);
-    else
-      k_msm_digits<4, false><<<nb, 256, 0, st>>>(d_scalars, p, w.counts.as<uint32_t>(), nullptr, nullptr, nullptr);
+  int ph = pf ? pf->begin(st, "msm_sort", n) : -1;   // group (point, window) entries by bucket
+  if (msm_sort_mode() == 0) {
+    // rocPRIM radix sort on ceil(log2(G + 1)) key bits
+    unsigned end_bit = 1;
+    while ((1ull << end_bit) <= p.G) end_bit++;
+    w.key_in.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
+    w.ent_in.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
+    size_t tmp_bytes = 0;
+    sort_pairs_u32(nullptr, tmp_bytes, nullptr, nullptr, nullptr, nullptr, M, end_bit, st);
+    w.sort_tmp.ensure(tmp_bytes);
+    if (n) {
+      const uint32_t nb = ceil_div(n, 256);
+      if (sw == 1)
+        k_msm_keys<1><<<nb, 256, 0, st>>>(d_scalars, p, w.key_in.as<uint32_t>(), w.ent_in.as<uint32_t>());
+      else
+        k_msm_keys<4><<<nb, 256, 0, st>>>(d_scalars, p, w.key_in.as<uint32_t>(), w.ent_in.as<uint32_t>());
+      ZK_LAUNCH_CHECK();
+      sort_pairs_u32(w.sort_tmp.p, tmp_bytes, w.key_in.as<uint32_t>(), w.key.as<uint32_t>(),
+                     w.ent_in.as<uint32_t>(), w.ent.as<uint32_t>(), M, end_bit, st);
+    }
+    k_msm_offsets<<<ceil_div(M + 1, 256), 256, 0, st>>>(w.key.as<uint32_t>(), (uint32_t)M, p.G, w.off.as<uint32_t>());
     ZK_LAUNCH_CHECK();
-  }
-  k_scan_local<<<nblk, 256, 0, st>>>(w.counts.as<uint32_t>(), p.G, w.scan_part.as<uint32_t>());
-  ZK_LAUNCH_CHECK();
-  k_scan_part<<<1, 1024, 0, st>>>(w.scan_part.as<uint32_t>(), nblk);
-  ZK_LAUNCH_CHECK();
-  k_scan_down<<<nblk, 256, 0, st>>>(w.counts.as<uint32_t>(), p.G, w.scan_part.as<uint32_t>(),
-                                    w.off.as<uint32_t>(), w.cursor.as<uint32_t>());
-  ZK_LAUNCH_CHECK();
-  if (n) {
-    const uint32_t nb = ceil_div(n, 256);
-    if (sw == 1)
-      k_msm_digits<1, true><<<nb, 256, 0, st>>>(d_scalars, p, nullptr, w.cursor.as<uint32_t>(),
-                                                w.ent.as<uint32_t>(), w.key.as<uint32_t>());
-    else
-      k_msm_digits<4, true><<<nb, 256, 0, st>>>(d_scalars, p, nullptr, w.cursor.as<uint32_t>(),
-                                                w.ent.as<uint32_t>(), w.key.as<uint32_t>());
+  } else {
+    // counting sort: global-atomic histogram, scan, scatter
+    if (w.counts.bytes < sizeof(uint32_t) * (p.G + 1)) {   // zero once; k_scan_down re-zeroes
+      w.counts.ensure(sizeof(uint32_t) * (p.G + 1));
+      ZK_HIP(hipMemsetAsync(w.counts.p, 0, w.counts.bytes, st));
+    }
+    w.cursor.ensure(sizeof(uint32_t) * (p.G + 1));
+    w.scan_part.ensure(sizeof(uint32_t) * nblk);
+    if (n) {
+      const uint32_t nb = ceil_div(n, 256);
+      if (sw == 1)
+        k_msm_digits<1, false><<<nb, 256, 0, st>>>(d_scalars, p, w.counts.as<uint32_t>(), nullptr, nullptr, nullptr);
+      else
+        k_msm_digits<4, false><<<nb, 256, 0, st>>>(d_scalars, p, w.counts.as<uint32_t>(), nullptr, nullptr, nullptr);
+      ZK_LAUNCH_CHECK();
+    }
+    k_scan_local<<<nblk, 256, 0, st>>>(w.counts.as<uint32_t>(), p.G, w.scan_part.as<uint32_t>());
     ZK_LAUNCH_CHECK();
+    k_scan_part<<<1, 1024, 0, st>>>(w.scan_part.as<uint32_t>(), nblk);
+    ZK_LAUNCH_CHECK();
+    k_scan_down<<<nblk, 256, 0, st>>>(w.counts.as<uint32_t>(), p.G, w.scan_part.as<uint32_t>(),
+                                      w.off.as<uint32_t>(), w.cursor.as<uint32_t>());
+    ZK_LAUNCH_CHECK();
+    if (n) {
+      const uint32_t nb = ceil_div(n, 256);
+      if (sw == 1)
+        k_msm_digits<1, true><<<nb, 256, 0, st>>>(d_scalars, p, nullptr, w.cursor.as<uint32_t>(),
+                                                  w.ent.as<uint32_t>(), w.key.as<uint32_t>());
+      else
+        k_msm_digits<4, true><<<nb, 256, 0, st>>>(d_scalars, p, nullptr, w.cursor.as<uint32_t>(),
+                                                  w.ent.as<uint32_t>(), w.key.as<uint32_t>());
+      ZK_LAUNCH_CHECK();
+    }
   }
   if (pf) pf->end(st, ph);
   // The number of non-zero digits M' <= M is known on device only: the T

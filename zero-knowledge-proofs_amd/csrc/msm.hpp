@@ -70,6 +70,7 @@ MsmPlan msm_make_plan(uint32_t n, int bits, int sw, int force_c = 0);
 // Device workspace of one in-flight MSM.
 struct MsmWork {
   DevBuf counts, off, cursor, scan_part, ent, key, buckets, partials, partials2, rc, res;
+  DevBuf key_in, ent_in, sort_tmp;   // radix-sort path
   PinnedBuf host_res;
   MsmPlan plan{};
   Prof* prof = nullptr;  // optional live kernel timing

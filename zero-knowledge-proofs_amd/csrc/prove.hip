@@ -15,7 +15,9 @@
 // away at upload (they contribute nothing), and only s*pi_A + r*B_1 -- which
 // depend on this proof's own MSM outputs -- are formed on the host.
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <thread>
 
 #include "ctx.hpp"
 
@@ -279,9 +281,12 @@ zk_pk_dev* pk_upload(zk_ctx* ctx, const zk_pk* pk, const zk_r1cs_csr* q, uint32_
 }
 
 // ---------------------------------------------------------------- prove ---
-// Partial accumulators of one shard (host XYZZ, Montgomery).
+// Partial accumulators of one shard (host XYZZ, Montgomery).  SC = s A + r B1
+// of this shard's A / B1 sums: by linearity the shards' SC add up to the
+// s pi_A + r B_1 of pi_C (core:224-265), so each rank pays for its own two
+// scalar multiplications while its H MSM is still running.
 struct Partial {
-  host::X<host::Fq> A, B1, IC, H;
+  host::X<host::Fq> A, B1, IC, H, SC;
   host::X<host::Fq2> B2;
   int32_t status;
 };
@@ -330,8 +335,12 @@ static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipS
 
 static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, const zk_fr* r,
                              const zk_fr* s) {
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+  const auto t_start = clk::now();
   hipStream_t st = ctx->stream;
   ctx->flags.ensure(16);
+  const int ph_span = ctx->prof.begin(st, "prove_gpu_span", pk->n);   // first kernel .. last MSM done
   ZK_HIP(hipMemsetAsync(ctx->flags.p, 0, 16, st));
   // The five MSMs are independent.  Streams (<= GPU_MAX_HW_QUEUES = 4, so no
   // two share a hardware queue): main (high priority) runs the quotient and
@@ -373,42 +382,75 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
     }
   };
   for (int k = 0; k < NUM_SIDE; k++) ZK_HIP(hipStreamWaitEvent(ctx->side[k], ctx->ev_scal, 0));
-  for (int slot : {MSM_B2, MSM_IC, MSM_A, MSM_B1}) launch_slot(slot);
+  for (int slot : {MSM_B2, MSM_IC, MSM_A, MSM_B1}) {
+    launch_slot(slot);
+    ZK_HIP(hipEventRecord(ctx->ev_done[slot], stream_of(slot)));
+  }
   quotient(ctx, pk, d_z, st);  // (Az, Bz, Cz) -> lo64(H) in tmp_scal, then H on the same stream
+  ctx->flags_host.ensure(16);
+  ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
   launch_slot(MSM_H);
-  uint32_t flags = 0;
-  ZK_HIP(hipMemcpyAsync(&flags, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
+  ZK_HIP(hipEventRecord(ctx->ev_done[MSM_H], st));
+  if (ph_span >= 0) {
+    for (int slot : {MSM_B2, MSM_IC, MSM_A, MSM_B1}) ZK_HIP(hipStreamWaitEvent(st, ctx->ev_done[slot], 0));
+    ctx->prof.end(st, ph_span);
+  }
+
+  // Host tails (Horner over each MSM's window partials, then s A + r B1) run
+  // as each MSM's stream reaches its event, overlapping the MSMs still on
+  // the GPU -- the H MSM, queued behind the quotient, usually finishes last.
+  ctx->prof.add_host("host_launch", ms_since(t_start));
+  double t_fin = 0;
+  Partial p{};
+  bool done[NUM_MSM] = {}, sc_done = false;
+  for (int left = NUM_MSM; left > 0;) {
+    bool progressed = false;
+    for (int slot = 0; slot < NUM_MSM; slot++) {
+      if (done[slot]) continue;
+      const hipError_t q = hipEventQuery(ctx->ev_done[slot]);
+      if (q == hipErrorNotReady) continue;
+      ZK_HIP(q);
+      const auto t_f = clk::now();
+      switch (slot) {
+        case MSM_A: p.A = msm_finish<G1>(ctx->msm[slot]); break;
+        case MSM_B2: p.B2 = msm_finish<G2>(ctx->msm[slot]); break;
+        case MSM_B1: p.B1 = msm_finish<G1>(ctx->msm[slot]); break;
+        case MSM_IC: p.IC = msm_finish<G1>(ctx->msm[slot]); break;
+        case MSM_H: p.H = msm_finish<G1>(ctx->msm[slot]); break;
+      }
+      done[slot] = progressed = true;
+      left--;
+      if (!sc_done && done[MSM_A] && done[MSM_B1]) {
+        p.SC = host::mul2_scalar(p.A, s->l, p.B1, r->l);
+        sc_done = true;
+      }
+      t_fin += ms_since(t_f);
+      if (left == 0) ctx->prof.add_host("host_tail_after_last", ms_since(t_f));
+    }
+    if (!progressed) std::this_thread::yield();
+  }
   for (int k = 0; k < NUM_SIDE; k++) ZK_HIP(hipStreamSynchronize(ctx->side[k]));
   ZK_HIP(hipStreamSynchronize(st));
+  ctx->prof.add_host("host_finish", t_fin);
   ctx->prof.collect();
-  Partial p{};
+  const uint32_t flags = *ctx->flags_host.as<uint32_t>();
   p.status = ZK_OK;
   if (flags & 5u) p.status = ZK_ERR_INVALID_WITNESS;
   else if (flags & 2u) p.status = ZK_ERR_QAP_DIVISION;
-  if (p.status != ZK_OK) return p;
-  p.A = msm_finish<G1>(ctx->msm[MSM_A]);
-  p.B2 = msm_finish<G2>(ctx->msm[MSM_B2]);
-  p.B1 = msm_finish<G1>(ctx->msm[MSM_B1]);
-  p.IC = msm_finish<G1>(ctx->msm[MSM_IC]);
-  p.H = msm_finish<G1>(ctx->msm[MSM_H]);
   return p;
 }
 
-static int combine(const Partial* parts, size_t k, const zk_fr* r, const zk_fr* s, zk_proof* out) {
+static int combine(const Partial* parts, size_t k, zk_proof* out) {
   for (size_t i = 0; i < k; i++)
     if (parts[i].status != ZK_OK) return parts[i].status;
-  auto A = host::inf<host::Fq>(), B1 = A, IC = A, H = A;
+  auto A = host::inf<host::Fq>(), C = A;
   auto B2 = host::inf<host::Fq2>();
   for (size_t i = 0; i < k; i++) {
     A = host::addp(A, parts[i].A);
-    B1 = host::addp(B1, parts[i].B1);
-    IC = host::addp(IC, parts[i].IC);
-    H = host::addp(H, parts[i].H);
     B2 = host::addp(B2, parts[i].B2);
+    // pi_C = IC + H_1 + s pi_A + r B_1 (core:224-265; identity terms add nothing)
+    C = host::addp(C, host::addp(host::addp(parts[i].IC, parts[i].H), parts[i].SC));
   }
-  // pi_C = IC + H_1 + s pi_A + r B_1 (core:224-265; identity terms add nothing)
-  auto C = host::addp(host::addp(IC, H),
-                      host::addp(host::mul_scalar(A, s->l), host::mul_scalar(B1, r->l)));
   host_to_abi<G1>(A, reinterpret_cast<uint64_t*>(&out->a));
   host_to_abi<G2>(B2, reinterpret_cast<uint64_t*>(&out->b));
   host_to_abi<G1>(C, reinterpret_cast<uint64_t*>(&out->c));
@@ -422,7 +464,7 @@ int prove_impl(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, size_t zlen, s
   if (zlen != pk->V) return ZK_ERR_INVALID_WITNESS;
   if (pk->nshards != 1) return ZK_ERR_ARG;
   Partial p = prove_partial(ctx, pk, reinterpret_cast<const uint64_t*>(d_z), r, s);
-  return combine(&p, 1, r, s, out);
+  return combine(&p, 1, out);
 }
 
 int prove_partial_impl(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, size_t zlen, size_t num_public,
@@ -441,7 +483,9 @@ int prove_partial_impl(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, size_t
 int combine_impl(const zk_prove_partial* parts, size_t k, const zk_fr* r, const zk_fr* s, zk_proof* out) {
   std::vector<Partial> ps(k);
   for (size_t i = 0; i < k; i++) std::memcpy(&ps[i], parts[i].bytes, sizeof(Partial));
-  return combine(ps.data(), k, r, s, out);
+  (void)r;
+  (void)s;
+  return combine(ps.data(), k, out);
 }
 
 }  // namespace zk

@@ -56,7 +56,16 @@ struct zk_pk_dev {
   uint32_t count[zk::NUM_MSM] = {};  // compacted bases (without extras)
   uint32_t extras[zk::NUM_MSM] = {}; // extra bases appended (shard 0 only)
   uint32_t h_lo = 0, h_hi = 0;       // H coefficient range of this shard
+  // Window-shifted base copies (msm_precompute_windows): bases[slot] holds
+  // win x (count + extras) points, window w = 2^(win_c w) x the base.
+  int win = 1, win_c = 0;
 };
+
+namespace zk {
+// Expand every slot's bases into the window-shifted copies the shared-bucket
+// MSM reads (ZK_MSM_PRECOMP=0 keeps one copy and per-window buckets).
+void pk_precompute_windows(zk_ctx* ctx, zk_pk_dev& pk);
+}
 
 struct zk_msm_bases {
   int device = 0;

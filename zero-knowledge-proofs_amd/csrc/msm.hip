@@ -15,19 +15,22 @@ MsmPlan msm_make_plan(uint32_t n, int bits, int sw, int force_c) {
   p.n = n;
   p.bits = bits;
   p.sw = sw;
+  // balanced windows only: for each window count the smallest c that covers
+  // the bits (a tiny top window would pile every point into a few huge buckets)
   int best_c = 4;
   double best = 1e300;
-  for (int c = 4; c <= 16; c++) {
-    int nwin = (bits + c - 1) / c;
-    if (nwin > MSM_MAXWIN) continue;
-    int top = bits - c * (nwin - 1);
-    double nbuck = (double)(nwin - 1) * (1u << (c - 1)) + (double)(1u << top);
+  for (int nw = (bits + 15) / 16; nw <= std::min(MSM_MAXWIN, bits); nw++) {
+    const int c = (bits + nw - 1) / nw;
+    if (c < 4) break;
+    const int nwin = (bits + c - 1) / c;
+    const int top = bits - c * (nwin - 1);
+    const double nbuck = (double)(nwin - 1) * (1u << (c - 1)) + (double)(1u << top);
     // accumulate: one mixed add per (point, window); reduce: ~2.5 full adds per bucket
-    double cost = (double)n * nwin + 3.5 * nbuck;
+    const double cost = (double)n * nwin + 3.5 * nbuck;
     if (cost < best) { best = cost; best_c = c; }
   }
   if (force_c) best_c = force_c;
-  // tuning overrides (tools/phase_bench.py sweeps): ZK_MSM_C, ZK_MSM_K
+  // tuning override (tools/phase_bench.py sweeps)
   if (const char* e = getenv("ZK_MSM_C")) best_c = std::max(4, std::min(16, atoi(e)));
   p.c = best_c;
   p.nwin = (bits + p.c - 1) / p.c;
@@ -52,6 +55,31 @@ MsmPlan msm_make_plan(uint32_t n, int bits, int sw, int force_c) {
   p.G = G;
   p.nrc = rc;
   p.nq = q;
+  p.nred = p.nwin;
+  p.shared = 0;
+  return p;
+}
+
+MsmPlan msm_make_plan_shared(uint32_t n, int bits, int sw, int c) {
+  MsmPlan p{};
+  p.n = n;
+  p.bits = bits;
+  p.sw = sw;
+  p.c = c;
+  p.nwin = (bits + c - 1) / c;
+  const int top = bits - c * (p.nwin - 1);
+  const int k = std::max(c - 1, top);   // signed digits <= 2^(c-1); the top window unsigned <= 2^top
+  p.shared = 1;
+  p.nred = 1;
+  p.nb[0] = 1u << k;
+  p.kr[0] = (uint8_t)(k / 2);
+  p.kc[0] = (uint8_t)(k - k / 2);
+  p.boff[0] = 0;
+  p.boff[1] = p.G = p.nb[0];
+  p.rcoff[0] = 0;
+  p.rcoff[1] = p.nrc = (1u << p.kr[0]) + (1u << p.kc[0]);
+  p.qoff[0] = 0;
+  p.qoff[1] = p.nq = p.kr[0] + p.kc[0] + 1;
   return p;
 }
 
@@ -156,8 +184,8 @@ __global__ void __launch_bounds__(256) k_msm_keys(const uint64_t* __restrict__ s
       carry = 0;
     }
     const size_t o = (size_t)w * p.n + i;
-    key[o] = mag ? p.boff[w] + mag - 1 : p.G;
-    ent[o] = i | (neg ? 0x80000000u : 0u);
+    key[o] = mag ? (p.shared ? 0u : p.boff[w]) + mag - 1 : p.G;
+    ent[o] = (p.shared ? (uint32_t)o : i) | (neg ? 0x80000000u : 0u);   // shared: base 2^(c w) P_i at w n + i
   }
 }
 
@@ -506,11 +534,10 @@ static uint32_t accum_threads() {
 }
 
 template <class C>
-void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scalars, int sw, uint32_t n,
-                int bits, hipStream_t st) {
+static void msm_launch_impl(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scalars, int sw,
+                            uint32_t n, hipStream_t st) {
   using X = typename C::X;
   MsmPlan& p = w.plan;
-  p = msm_make_plan(n, bits, sw);
   if (p.G > (uint32_t)MSM_SCAN_BLOCK * 1024) throw Error(ZK_ERR_ARG, "msm: too many buckets");
   const size_t M = (size_t)n * p.nwin;
   if (M >= 0x80000000ull) throw Error(ZK_ERR_ARG, "msm: too many (point, window) entries");
@@ -530,7 +557,7 @@ void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scal
   Prof* pf = w.prof;
   const bool g2 = sizeof(typename C::A) == sizeof(G2A);
   int ph = pf ? pf->begin(st, "msm_sort", n) : -1;   // group (point, window) entries by bucket
-  if (msm_sort_mode() == 0) {
+  if (msm_sort_mode() == 0 || p.shared) {
     // rocPRIM radix sort on ceil(log2(G + 1)) key bits
     unsigned end_bit = 1;
     while ((1ull << end_bit) <= p.G) end_bit++;
@@ -623,6 +650,96 @@ void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scal
 }
 
 template <class C>
+void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scalars, int sw, uint32_t n,
+                int bits, hipStream_t st) {
+  w.plan = msm_make_plan(n, bits, sw);
+  msm_launch_impl<C>(w, d_bases, d_scalars, sw, n, st);
+}
+
+template <class C>
+void msm_launch_shared(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scalars, int sw, uint32_t n,
+                       int bits, int c, hipStream_t st) {
+  w.plan = msm_make_plan_shared(n, bits, sw, c);
+  if ((uint64_t)n * w.plan.nwin >= 0x80000000ull) throw Error(ZK_ERR_ARG, "msm: too many window bases");
+  msm_launch_impl<C>(w, d_bases, d_scalars, sw, n, st);
+}
+
+// ------------------------------------------- precomputed window bases -----
+constexpr int NORM_CHUNK = 16;
+template <class C>
+__global__ void __launch_bounds__(128) k_normalize(const typename C::X* __restrict__ in, size_t n,
+                                                   typename C::F* __restrict__ pre,
+                                                   typename C::A* __restrict__ out) {
+  using F = typename C::F;
+  const size_t c0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * NORM_CHUNK;
+  if (c0 >= n) return;
+  const size_t c1 = min(c0 + NORM_CHUNK, n);
+  F run;
+  f_set_one(run);
+  for (size_t j = c0; j < c1; j++) {
+    pre[j] = run;
+    const F z = ld_vec(&in[j]).ZZZ;
+    if (!f_is_zero(z)) run = f_mul(run, z);
+  }
+  F inv = f_inv(run);
+  for (size_t j = c1; j-- > c0;) {
+    const typename C::X q = ld_vec(&in[j]);
+    typename C::A a;
+    if (f_is_zero(q.ZZZ)) {
+      f_set_zero(a.x);
+      f_set_zero(a.y);
+    } else {
+      const F i3 = f_mul(inv, pre[j]);   // ZZZ^-1 = Z^-3
+      inv = f_mul(inv, q.ZZZ);
+      const F zi = f_mul(q.ZZ, i3);      // Z^-1
+      a.x = f_mul(q.X, f_sqr(zi));
+      a.y = f_mul(q.Y, i3);
+    }
+    st_vec(&out[j], a);
+  }
+}
+
+template <class C>
+void batch_normalize(const typename C::X* d_in, size_t n, typename C::F* d_pre, typename C::A* d_out,
+                     hipStream_t st) {
+  if (!n) return;
+  k_normalize<C><<<ceil_div(ceil_div(n, NORM_CHUNK), 128), 128, 0, st>>>(d_in, n, d_pre, d_out);
+  ZK_LAUNCH_CHECK();
+}
+
+// out[i] = 2^c in[i] (XYZZ)
+template <class C>
+__global__ void __launch_bounds__(128) k_shift_bases(const typename C::A* __restrict__ in, size_t n, int c,
+                                                     typename C::X* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const typename C::A a = ld_vec(&in[i]);
+  typename C::X q;
+  if (aff_is_inf(a)) {
+    xyzz_set_inf(q);
+  } else {
+    q = aff_dbl(a);
+    for (int k = 1; k < c; k++) q = xyzz_dbl(q);
+  }
+  st_vec(&out[i], q);
+}
+
+template <class C>
+void msm_precompute_windows(typename C::A* d_bases, size_t n, int W, int c, hipStream_t st) {
+  if (!n || W < 2) return;
+  DevBuf xs, pre;
+  xs.ensure(sizeof(typename C::X) * n);
+  pre.ensure(sizeof(typename C::F) * n);
+  for (int w = 1; w < W; w++) {
+    k_shift_bases<C><<<ceil_div(n, 128), 128, 0, st>>>(d_bases + (size_t)(w - 1) * n, n, c,
+                                                        xs.as<typename C::X>());
+    ZK_LAUNCH_CHECK();
+    batch_normalize<C>(xs.as<typename C::X>(), n, pre.as<typename C::F>(), d_bases + (size_t)w * n, st);
+  }
+  ZK_HIP(hipStreamSynchronize(st));   // xs / pre die here
+}
+
+template <class C>
 void msm_download(MsmWork& w, hipStream_t st) {
   using X = typename C::X;
   const size_t bytes = sizeof(X) * w.plan.nq;
@@ -641,14 +758,17 @@ host::X<typename C::HF> msm_finish(const MsmWork& w) {
   static_assert(sizeof(HX) == sizeof(typename C::X), "layout");
   const MsmPlan& p = w.plan;
   const HX* r = w.host_res.as<const HX>();
+  // reduction window `win` carries weight 2^(c win); a shared plan has one
+  // window of weight 1 (the shifts live in the precomputed bases)
+  auto wexp = [&](int win) { return p.shared ? 0 : p.c * win; };
   int maxe = 0;
-  for (int win = 0; win < p.nwin; win++)
-    maxe = std::max(maxe, p.c * win + std::max<int>(p.kc[win] + p.kr[win] - 1, p.kc[win]));
+  for (int win = 0; win < (int)p.nred; win++)
+    maxe = std::max(maxe, wexp(win) + std::max<int>(p.kc[win] + p.kr[win] - 1, p.kc[win]));
   std::vector<std::vector<const HX*>> at(maxe + 1);
-  for (int win = 0; win < p.nwin; win++) {
+  for (int win = 0; win < (int)p.nred; win++) {
     const int kr = p.kr[win], kc = p.kc[win];
     for (int q = 0; q < kr + kc + 1; q++) {
-      int e = q < kr ? p.c * win + kc + q : q < kr + kc ? p.c * win + (q - kr) : p.c * win;
+      int e = q < kr ? wexp(win) + kc + q : q < kr + kc ? wexp(win) + (q - kr) : wexp(win);
       at[e].push_back(&r[p.qoff[win] + q]);
     }
   }
@@ -736,6 +856,10 @@ void host_to_abi<G2>(const host::X<host::Fq2>& p, uint64_t* w) {
 
 #define ZK_MSM_INST(C)                                                                               \
   template void msm_launch<C>(MsmWork&, const C::A*, const uint64_t*, int, uint32_t, int, hipStream_t); \
+  template void msm_launch_shared<C>(MsmWork&, const C::A*, const uint64_t*, int, uint32_t, int, int,   \
+                                     hipStream_t);                                                    \
+  template void msm_precompute_windows<C>(C::A*, size_t, int, int, hipStream_t);                       \
+  template void batch_normalize<C>(const C::X*, size_t, C::F*, C::A*, hipStream_t);                    \
   template void msm_download<C>(MsmWork&, hipStream_t);                                              \
   template host::X<C::HF> msm_finish<C>(const MsmWork&);                                            \
   template void convert_bases<C>(const uint64_t*, C::A*, size_t, hipStream_t);                       \

@@ -63,9 +63,16 @@ struct MsmPlan {
   uint8_t kr[MSM_MAXWIN], kc[MSM_MAXWIN];   // nb = 2^(kr + kc): rows x columns
   uint32_t rcoff[MSM_MAXWIN + 1];   // first row/col sum of window w (rows, then columns)
   uint32_t qoff[MSM_MAXWIN + 1];    // first quantity of window w (U^C, U^D, P)
+  uint32_t nred;                    // reduction windows (nwin, or 1 when shared)
+  int shared;                       // windows share one bucket set (precomputed 2^(c w) P bases)
 };
 
 MsmPlan msm_make_plan(uint32_t n, int bits, int sw, int force_c = 0);
+// Window-shared plan: digit window w of point i uses the precomputed base
+// 2^(c w) P_i (msm_precompute_windows), so every window accumulates into
+// ONE set of 2^max(c-1, top) buckets -- the bucket reduction shrinks by the
+// window count and the per-window Horner disappears.
+MsmPlan msm_make_plan_shared(uint32_t n, int bits, int sw, int c);
 
 // Device workspace of one in-flight MSM.
 struct MsmWork {
@@ -81,6 +88,19 @@ struct MsmWork {
 template <class C>
 void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scalars, int sw,
                 uint32_t n, int bits, hipStream_t st);
+// Same over window-shifted bases: d_bases holds nwin x n points, window-major.
+template <class C>
+void msm_launch_shared(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scalars, int sw,
+                       uint32_t n, int bits, int c, hipStream_t st);
+// d_bases[w n + i] = 2^(c w) d_bases[i] for 0 < w < W (the first n are given;
+// capacity W n).  One-time, at proving-key upload.
+template <class C>
+void msm_precompute_windows(typename C::A* d_bases, size_t n, int W, int c, hipStream_t st);
+// XYZZ -> affine for n points with one Fermat inversion per 16-point chunk
+// (pre: n field elements of scratch).
+template <class C>
+void batch_normalize(const typename C::X* d_in, size_t n, typename C::F* d_pre, typename C::A* d_out,
+                     hipStream_t st);
 // Copy the per-window partials back (async) -- call msm_finish after a sync.
 template <class C>
 void msm_download(MsmWork& w, hipStream_t st);

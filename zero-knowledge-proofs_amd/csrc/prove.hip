@@ -277,7 +277,33 @@ zk_pk_dev* pk_upload(zk_ctx* ctx, const zk_pk* pk, const zk_r1cs_csr* q, uint32_
     upload_vector<G1>(*d, MSM_H, pk->h_g1, lo, hi, 0, none1, st);
   }
   // the a/b vectors may be shorter than V (core:171 `i < pk.a_g1.len()`): indices stay < V.
+  pk_precompute_windows(ctx, *d);
   return d.release();
+}
+
+// The prove MSMs all take 64-bit scalars (lo64, core:156-161 / 203-208, and
+// the u64 limbs of r, s against 2^(64k) delta): c = 16 gives 4 windows whose
+// shifted bases 2^16 P, 2^32 P, 2^48 P are computed once here, so each MSM
+// sums into one set of 2^16 buckets instead of 3 x 2^15 + 2^16.
+constexpr int PROVE_WIN_C = 16, PROVE_WIN = 4;
+
+void pk_precompute_windows(zk_ctx* ctx, zk_pk_dev& pk) {
+  const char* e = getenv("ZK_MSM_PRECOMP");
+  if (e && std::strcmp(e, "0") == 0) return;
+  hipStream_t st = ctx->stream;
+  for (int slot = 0; slot < NUM_MSM; slot++) {
+    const size_t n = (size_t)pk.count[slot] + pk.extras[slot];
+    const size_t asz = slot == MSM_B2 ? sizeof(G2A) : sizeof(G1A);
+    DevBuf big;
+    big.ensure(asz * std::max<size_t>(n * PROVE_WIN, 1));
+    if (n) ZK_HIP(hipMemcpyAsync(big.p, pk.bases[slot].p, asz * n, hipMemcpyDeviceToDevice, st));
+    if (slot == MSM_B2) msm_precompute_windows<G2>(big.as<G2A>(), n, PROVE_WIN, PROVE_WIN_C, st);
+    else msm_precompute_windows<G1>(big.as<G1A>(), n, PROVE_WIN, PROVE_WIN_C, st);
+    ZK_HIP(hipStreamSynchronize(st));
+    pk.bases[slot] = std::move(big);
+  }
+  pk.win = PROVE_WIN;
+  pk.win_c = PROVE_WIN_C;
 }
 
 // ---------------------------------------------------------------- prove ---
@@ -374,10 +400,18 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
     }
     const uint32_t n = cnt + nex;
     if (slot == MSM_B2) {
-      msm_launch<G2>(ctx->msm[slot], pk->bases[slot].as<G2A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64, ss);
+      if (pk->win > 1)
+        msm_launch_shared<G2>(ctx->msm[slot], pk->bases[slot].as<G2A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64,
+                              pk->win_c, ss);
+      else
+        msm_launch<G2>(ctx->msm[slot], pk->bases[slot].as<G2A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64, ss);
       msm_download<G2>(ctx->msm[slot], ss);
     } else {
-      msm_launch<G1>(ctx->msm[slot], pk->bases[slot].as<G1A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64, ss);
+      if (pk->win > 1)
+        msm_launch_shared<G1>(ctx->msm[slot], pk->bases[slot].as<G1A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64,
+                              pk->win_c, ss);
+      else
+        msm_launch<G1>(ctx->msm[slot], pk->bases[slot].as<G1A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64, ss);
       msm_download<G1>(ctx->msm[slot], ss);
     }
   };

@@ -178,41 +178,6 @@ __global__ void __launch_bounds__(128) k_fixed_base(const typename C::A* __restr
   st_vec(&out[i], acc);
 }
 
-// XYZZ -> affine (Montgomery), batch inversion of ZZZ per thread chunk.
-constexpr int NORM_CHUNK = 16;
-template <class C>
-__global__ void __launch_bounds__(128) k_normalize(const typename C::X* __restrict__ in, size_t n,
-                                                   typename C::F* __restrict__ pre,
-                                                   typename C::A* __restrict__ out) {
-  using F = typename C::F;
-  const size_t c0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * NORM_CHUNK;
-  if (c0 >= n) return;
-  const size_t c1 = min(c0 + NORM_CHUNK, n);
-  F run;
-  f_set_one(run);
-  for (size_t j = c0; j < c1; j++) {
-    pre[j] = run;
-    const F z = ld_vec(&in[j]).ZZZ;
-    if (!f_is_zero(z)) run = f_mul(run, z);
-  }
-  F inv = f_inv(run);
-  for (size_t j = c1; j-- > c0;) {
-    const typename C::X p = ld_vec(&in[j]);
-    typename C::A a;
-    if (f_is_zero(p.ZZZ)) {
-      f_set_zero(a.x);
-      f_set_zero(a.y);
-    } else {
-      const F i3 = f_mul(inv, pre[j]);   // ZZZ^-1 = Z^-3
-      inv = f_mul(inv, p.ZZZ);
-      const F zi = f_mul(p.ZZ, i3);      // Z^-1
-      a.x = f_mul(p.X, f_sqr(zi));
-      a.y = f_mul(p.Y, i3);
-    }
-    st_vec(&out[j], a);
-  }
-}
-
 // device affine (Montgomery, (0,0) = infinity) -> canonical ABI words
 __device__ __forceinline__ void st_canon(uint64_t* w, const Fq& m) {
   Fq c = fp_from_mont(m);
@@ -294,9 +259,7 @@ static void fixed_base(zk_ctx* ctx, const uint64_t* d_scal, const uint32_t* d_id
   k_fixed_base<C><<<ceil_div(n, 128), 128, 0, st>>>(T.dev.template as<typename C::A>(), d_scal, d_idx, n,
                                                      xs.template as<typename C::X>());
   ZK_LAUNCH_CHECK();
-  k_normalize<C><<<ceil_div(ceil_div(n, NORM_CHUNK), 128), 128, 0, st>>>(xs.template as<typename C::X>(), n,
-                                                                         pre.template as<typename C::F>(), d_out);
-  ZK_LAUNCH_CHECK();
+  batch_normalize<C>(xs.template as<typename C::X>(), n, pre.template as<typename C::F>(), d_out, st);
   ZK_HIP(hipStreamSynchronize(st));  // xs / pre die here
 }
 
@@ -575,6 +538,7 @@ int setup_impl(zk_ctx* ctx, const zk_r1cs_csr* q, const zk_setup_params* P, uint
   build_slot(MSM_H, false, hh, sh, n, 0, none, 0);
   d->h_lo = (uint32_t)(n * shard / nshards);
   d->h_hi = (uint32_t)(n * (shard + 1) / nshards);
+  pk_precompute_windows(ctx, *d);
   *pk_dev = d.release();
   return ZK_OK;
 }

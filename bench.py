@@ -8,9 +8,11 @@ plus G1 MSM scalar-point pairs/s at 2^20 (configs[1]) on rank 0.
 A step = one full prove (quotient NTTs + 5 MSMs + host tail) with the proving
 key and witness already resident in HBM.  N > 1: weak scaling -- the circuit
 has N * 2^log_n constraints, every rank holds 1/N of every base vector
-(GPU setup of its shard), replicates the quotient, runs its MSM shard, and
-the 1.5 KB partial accumulators meet in ONE all-gather over RCCL (the
-torch.distributed "nccl" backend) before the fold.  Rank 0 prints one JSON
+(GPU setup of its shard), computes its 1/N of the quotient
+(four-step transforms with three RCCL all-to-alls inside the library, H
+coefficients i = rank mod N), runs its MSM shard, and the 1.5 KB partial
+accumulators meet in ONE all-gather over RCCL (the torch.distributed "nccl"
+backend) before the fold.  Rank 0 prints one JSON
 line.  The CPU baseline leg times the C restatement (oracle/, single thread)
 on a bounded sample of the same workload.
 """
@@ -200,6 +202,13 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
 
     ctx = zkp.Context(local)
+    if dist:
+        # one RCCL communicator inside the library for the distributed
+        # quotient (three all-to-alls per proof over xGMI); the unique id
+        # travels over the torch process group
+        obj = [zkp.Context.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        ctx.attach_rccl(obj[0], rank, world)
     n = (1 << args.log_n) * world
     log_n_total = n.bit_length() - 1
     params, r, s = setup_params(args.seed)

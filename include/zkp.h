@@ -194,6 +194,23 @@ int zk_groth16_prove_partial(zk_ctx *ctx, const zk_pk_dev *pk_shard, const void 
 int zk_groth16_prove_combine(const zk_prove_partial *parts, size_t nparts,
                              const zk_fr *r, const zk_fr *s, zk_proof *out);
 
+/* The quotient of a sharded key, distributed: ranks attached to one RCCL
+ * communicator split every transform of compute_quotient_polynomial
+ * (crates/groth16-qap/src/lib.rs:225-271) four-step over xGMI -- three
+ * all-to-alls per proof -- instead of each recomputing it; shard k's H
+ * bases are the coefficients i = k mod nshards.  Used by
+ * zk_groth16_prove_partial when the ctx's communicator matches the key's
+ * (shard, nshards) and nshards is 2, 4 or 8; otherwise every rank computes
+ * the whole quotient.  No reference counterpart (multi-GPU). */
+int zk_rccl_unique_id(uint8_t out[128]);   /* one rank makes it, all attach with it */
+int zk_ctx_attach_rccl(zk_ctx *ctx, const uint8_t unique_id[128], int rank, int world);
+/* Diagnostic: nshards virtual ranks of one key on this ctx's single device
+ * (the all-to-alls become device copies) -- checks the distributed path's
+ * arithmetic and index maps without N devices. */
+int zk_test_prove_virtual_shards(zk_ctx *ctx, const zk_pk_dev *const *shards, uint32_t nshards,
+                                 const void *d_z, size_t zlen, size_t num_public, const zk_fr *r,
+                                 const zk_fr *s, zk_proof *out);
+
 /* ------------------------------------------------------ serialization --- */
 /* ark-serialize CanonicalSerialize, compressed (zcash flag bits), for
  * Proof (crates/groth16-core/src/lib.rs:28): a(48) | b(96) | c(48). */

@@ -108,3 +108,48 @@ def test_sharded_prove_equals_full(ctx, zkp, oracle, nshards):
         dpk = zkp.CRS.generate_device(ctx, qap, zkp.SetupParams(*params), 1, shard=k, nshards=nshards)
         parts.append(zkp.Prover.prove_partial(dpk, dz.data_ptr(), len(z), 1, r, s))
     assert np.array_equal(zkp.Prover.combine(parts, r, s).words, oproof)
+
+
+@pytest.mark.parametrize("nshards", [2, 4, 8])
+def test_distributed_quotient_virtual_ranks(ctx, zkp, oracle, nshards):
+    """The RCCL path's distributed quotient (four-step transforms, three
+    all-to-alls, H coefficients i = rank mod N per shard), run as N virtual
+    ranks on one device, gives the oracle's proof bit for bit."""
+    qap, csr_o, params, r, s, z = _synthetic(zkp, oracle, 10, 1700 + nshards)
+    rc, opk, _ = oracle.setup(csr_o, params, 1, nthreads=8)
+    rc, oproof = oracle.prove(opk, csr_o, z, 1, r, s)
+    import torch
+    dz = torch.from_numpy(z.view(np.int64).copy()).cuda()
+    pk = U.pk_from_oracle(zkp, opk, qap, 1)
+    dpks = [pk.upload(ctx, shard=k, nshards=nshards) for k in range(nshards)]
+    proof = zkp.Prover.prove_virtual_shards(dpks, dz.data_ptr(), len(z), 1, r, s)
+    assert np.array_equal(proof.words, oproof)
+    # device-side setup shards (strided H bases) give the same
+    dpks = [zkp.CRS.generate_device(ctx, qap, zkp.SetupParams(*params), 1, shard=k, nshards=nshards)
+            for k in range(nshards)]
+    assert np.array_equal(zkp.Prover.prove_virtual_shards(dpks, dz.data_ptr(), len(z), 1, r, s).words, oproof)
+
+
+def test_distributed_quotient_rejects_bad_witness(ctx, zkp, oracle):
+    """A witness failing the row-1 check on one rank's rows still reports
+    InvalidWitness; one failing another row reports PolynomialDivisionFailed."""
+    qap, csr_o, params, r, s, z = _synthetic(zkp, oracle, 8, 77)
+    import torch
+    rc, opk, _ = oracle.setup(csr_o, params, 1, nthreads=8)
+    pk = U.pk_from_oracle(zkp, opk, qap, 1)
+    dpks = [pk.upload(ctx, shard=k, nshards=4) for k in range(4)]
+    for var, err in ((6, zkp.InvalidWitness), (3 * 37 + 3, zkp.PolynomialDivisionFailed)):
+        zb = z.copy()
+        zb[var, 0] ^= 1          # z_{3j+3} = x_j y_j breaks row j (row 1 <-> variable 6)
+        dz = torch.from_numpy(zb.view(np.int64).copy()).cuda()
+        with pytest.raises(err):
+            zkp.Prover.prove_virtual_shards(dpks, dz.data_ptr(), len(zb), 1, r, s)
+
+
+def test_rccl_attach_single_rank(zkp):
+    """The library's RCCL communicator (used by sharded keys' distributed
+    quotient) initialises through the C ABI; world 1 needs no peers."""
+    uid = zkp.Context.rccl_unique_id()
+    assert len(uid) == 128
+    with zkp.Context(0) as c:
+        c.attach_rccl(uid, 0, 1)

@@ -40,7 +40,8 @@ EXPORTS = (
     "zk_groth16_setup", "zk_groth16_setup_dev", "zk_pk_upload", "zk_pk_free",
     "zk_groth16_prove", "zk_groth16_prove_dev", "zk_pk_upload_shard",
     "zk_groth16_setup_dev_shard", "zk_groth16_prove_partial", "zk_groth16_prove_combine",
-    "zk_proof_serialize_compressed",
+    "zk_proof_serialize_compressed", "zk_rccl_unique_id", "zk_ctx_attach_rccl",
+    "zk_test_prove_virtual_shards",
 )
 
 
@@ -222,6 +223,18 @@ class Context:
 
     def __exit__(self, *a):
         self.close()
+
+    # ---- RCCL communicator for the distributed quotient of sharded keys ----
+    @staticmethod
+    def rccl_unique_id():
+        buf = (C.c_uint8 * 128)()
+        _check(lib().zk_rccl_unique_id(buf), None, "zk_rccl_unique_id")
+        return bytes(buf)
+
+    def attach_rccl(self, unique_id, rank, world):
+        buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+        _check(lib().zk_ctx_attach_rccl(C.c_void_p(self._h), buf, C.c_int(rank), C.c_int(world)), self,
+               "zk_ctx_attach_rccl")
 
     # ---- live kernel timing (HIP events on the launching stream) ----
     def profile(self, enable=True):
@@ -643,6 +656,19 @@ class Prover:
                                             C.byref(_fr(s)), buf)
         _check(rc, ctx, "zk_groth16_prove_partial")
         return bytes(buf)
+
+    @staticmethod
+    def prove_virtual_shards(dpks, d_z_ptr, zlen, num_public, r, s):
+        """Diagnostic: the distributed quotient + sharded MSMs of len(dpks)
+        virtual ranks on one device (zk_test_prove_virtual_shards)."""
+        ctx = dpks[0].ctx
+        arr = (C.c_void_p * len(dpks))(*[C.c_void_p(d._h) for d in dpks])
+        out = _Proof()
+        rc = lib().zk_test_prove_virtual_shards(C.c_void_p(ctx._h), arr, C.c_uint32(len(dpks)),
+                                                C.c_void_p(d_z_ptr), C.c_size_t(zlen), C.c_size_t(num_public),
+                                                C.byref(_fr(r)), C.byref(_fr(s)), C.byref(out))
+        _check(rc, ctx, "zk_test_prove_virtual_shards")
+        return Proof._from_c(out)
 
     @staticmethod
     def combine(partials, r, s):

@@ -8,6 +8,8 @@
 namespace zk {
 zk_pk_dev* pk_upload(zk_ctx* ctx, const zk_pk* pk, const zk_r1cs_csr* q, uint32_t shard, uint32_t nshards);
 int prove_impl(zk_ctx*, const zk_pk_dev*, const void*, size_t, size_t, const zk_fr*, const zk_fr*, zk_proof*);
+int prove_virtual_shards_impl(zk_ctx*, const zk_pk_dev* const*, uint32_t, const void*, size_t, size_t,
+                              const zk_fr*, const zk_fr*, zk_proof*);
 int prove_partial_impl(zk_ctx*, const zk_pk_dev*, const void*, size_t, size_t, const zk_fr*, const zk_fr*,
                        zk_prove_partial*);
 int combine_impl(const zk_prove_partial*, size_t, const zk_fr*, const zk_fr*, zk_proof*);
@@ -363,6 +365,32 @@ int zk_groth16_prove_combine(const zk_prove_partial* parts, size_t nparts, const
   } catch (...) {
     return ZK_ERR_DEVICE;
   }
+}
+
+int zk_rccl_unique_id(uint8_t out[128]) {
+  if (!out) return ZK_ERR_ARG;
+  try {
+    rccl_unique_id(out);
+    return ZK_OK;
+  } catch (const Error& e) {
+    return e.code;
+  } catch (...) {
+    return ZK_ERR_RCCL;
+  }
+}
+
+int zk_ctx_attach_rccl(zk_ctx* ctx, const uint8_t unique_id[128], int rank, int world) {
+  if (!ctx || !unique_id || world < 1 || rank < 0 || rank >= world) return ZK_ERR_ARG;
+  ZK_GUARD(ctx, {
+    ctx->exch = make_rccl_exchange(unique_id, rank, world);
+    return ZK_OK;
+  })
+}
+
+int zk_test_prove_virtual_shards(zk_ctx* ctx, const zk_pk_dev* const* shards, uint32_t nshards, const void* d_z,
+                                 size_t zlen, size_t num_public, const zk_fr* r, const zk_fr* s, zk_proof* out) {
+  if (!ctx || !shards || !d_z || !r || !s || !out) return ZK_ERR_ARG;
+  ZK_GUARD(ctx, { return prove_virtual_shards_impl(ctx, shards, nshards, d_z, zlen, num_public, r, s, out); })
 }
 
 int zk_proof_serialize_compressed(const zk_proof* proof, uint8_t out[192]) {

@@ -6,6 +6,7 @@
 #include <string>
 #include <vector>
 
+#include "dist.hpp"
 #include "msm.hpp"
 #include "ntt.hpp"
 
@@ -39,6 +40,8 @@ struct zk_ctx {
   zk::DevBuf scal[zk::NUM_MSM];
   zk::DevBuf tmp_bases, tmp_scal, tmp_fr;
   zk::Prof prof;
+  std::unique_ptr<zk::Exchange> exch;          // RCCL communicator (sharded prover), if attached
+  zk::DistQ dq;                                // distributed-quotient buffers
 
   zk::NttDomain& domain(uint32_t log_n);
 };
@@ -55,7 +58,6 @@ struct zk_pk_dev {
   zk::DevBuf idx[zk::NUM_MSM];      // u32 variable index per compacted base (H: coefficient index)
   uint32_t count[zk::NUM_MSM] = {};  // compacted bases (without extras)
   uint32_t extras[zk::NUM_MSM] = {}; // extra bases appended (shard 0 only)
-  uint32_t h_lo = 0, h_hi = 0;       // H coefficient range of this shard
   // Window-shifted base copies (msm_precompute_windows): bases[slot] holds
   // win x (count + extras) points, window w = 2^(win_c w) x the base.
   int win = 1, win_c = 0;

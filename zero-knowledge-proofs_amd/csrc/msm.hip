@@ -556,7 +556,7 @@ static void msm_launch_impl(MsmWork& w, const typename C::A* d_bases, const uint
 
   Prof* pf = w.prof;
   const bool g2 = sizeof(typename C::A) == sizeof(G2A);
-  int ph = pf ? pf->begin(st, "msm_sort", n) : -1;   // group (point, window) entries by bucket
+  int ph = pf ? pf->begin(st, (w.tag + "msm_sort").c_str(), n) : -1;   // group (point, window) entries by bucket
   if (msm_sort_mode() == 0 || p.shared) {
     // rocPRIM radix sort on ceil(log2(G + 1)) key bits
     unsigned end_bit = 1;
@@ -616,14 +616,14 @@ static void msm_launch_impl(MsmWork& w, const typename C::A* d_bases, const uint
   // The number of non-zero digits M' <= M is known on device only: the T
   // accumulate threads split it evenly there (chunk_len), no host sync.
   if (M) {
-    ph = pf ? pf->begin(st, g2 ? "msm_accum_g2" : "msm_accum_g1", n) : -1;
+    ph = pf ? pf->begin(st, (w.tag + (g2 ? "msm_accum_g2" : "msm_accum_g1")).c_str(), n) : -1;
     k_msm_accum<C><<<ceil_div(p.T, 128), 128, 0, st>>>(d_bases, w.ent.as<uint32_t>(), w.key.as<uint32_t>(),
                                                         w.off.as<uint32_t>(), p.G, p.T, w.buckets.as<X>(),
                                                         w.partials.as<X>());
     ZK_LAUNCH_CHECK();
     if (pf) pf->end(st, ph);
   }
-  ph = pf ? pf->begin(st, "msm_merge", p.G) : -1;   // buckets split across chunks
+  ph = pf ? pf->begin(st, (w.tag + "msm_merge").c_str(), p.G) : -1;   // buckets split across chunks
   k_msm_fixup<C><<<ceil_div(p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), p.G, p.T, p.fix_max, w.buckets.as<X>(),
                                                       w.partials.as<X>());
   ZK_LAUNCH_CHECK();
@@ -640,7 +640,7 @@ static void msm_launch_impl(MsmWork& w, const typename C::A* d_bases, const uint
     }
   }
   if (pf) pf->end(st, ph);
-  ph = pf ? pf->begin(st, "msm_bucket_sum", p.G) : -1;   // row/col sums + quantities
+  ph = pf ? pf->begin(st, (w.tag + "msm_bucket_sum").c_str(), p.G) : -1;   // row/col sums + quantities
   k_msm_rowcol<C><<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.off.as<uint32_t>(),
                                                                                 w.buckets.as<X>(), w.rc.as<X>());
   ZK_LAUNCH_CHECK();

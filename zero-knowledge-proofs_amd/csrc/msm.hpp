@@ -25,6 +25,7 @@
 //              one Horner pass over ~16 nwin partials (latency-bound; see
 //              host_ec.hpp for why this tail runs on the host)
 #pragma once
+#include <string>
 #include <vector>
 
 #include "common.hpp"
@@ -81,6 +82,7 @@ struct MsmWork {
   PinnedBuf host_res;
   MsmPlan plan{};
   Prof* prof = nullptr;  // optional live kernel timing
+  std::string tag;       // phase-name prefix (per-MSM profiling)
 };
 
 // Launch the device part of an MSM over n Montgomery-affine device bases and

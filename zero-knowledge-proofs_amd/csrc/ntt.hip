@@ -8,26 +8,6 @@ namespace zk {
 
 constexpr int NTT_TILE_LOG = 11;  // 2048 elements x 32 B = 64 KiB of LDS per workgroup
 constexpr int NTT_THREADS = 256;
-constexpr int NTT_SM_LOG = 11;    // sub-transform twiddles: powers of omega_2048 (domain-independent)
-constexpr int NTT_TL_LOG = 12;    // omega_n^x = TL[x mod 4096] * TH[x / 4096]
-
-__device__ __forceinline__ uint32_t bitrev32(uint32_t x, uint32_t log_n) {
-  return log_n ? (__builtin_bitreverse32(x) >> (32 - log_n)) : 0;
-}
-
-struct NttTabs {
-  const Fr* sm;   // omega_2048^j, j < 1024 (or the inverse root)
-  const Fr* tl;   // omega_n^x, x < min(n, 4096)
-  const Fr* th;   // omega_n^(4096 y), y < n / 4096
-};
-
-// omega_n^x, x < n
-__device__ __forceinline__ Fr tw_full(const NttTabs& t, uint32_t x, uint32_t log_n) {
-  Fr w = ld_vec(&t.tl[x & ((1u << NTT_TL_LOG) - 1)]);
-  if (log_n > NTT_TL_LOG) w = fp_mul(w, ld_vec(&t.th[x >> NTT_TL_LOG]));
-  return w;
-}
-
 // One radix-2^R round of a tile's sub-transform: local stages
 // [lsb, lsb + R).  Each thread owns whole groups of 2^R elements (rows
 // r0 + m 2^lsb, one column), keeps them in registers for all R stages and
@@ -169,10 +149,6 @@ static std::vector<uint32_t> pass_plan(uint32_t L) {
   return ns;
 }
 
-static NttTabs tabs_of(const NttDomain& dom, bool inv) {
-  return inv ? NttTabs{dom.ism.as<Fr>(), dom.itl.as<Fr>(), dom.ith.as<Fr>()}
-             : NttTabs{dom.sm.as<Fr>(), dom.tl.as<Fr>(), dom.th.as<Fr>()};
-}
 
 void ntt_dif(Fr* d, const NttDomain& dom, bool inv, hipStream_t st, Prof* pf) {
   const uint32_t L = dom.log_n;

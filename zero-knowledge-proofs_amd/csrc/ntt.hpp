@@ -35,6 +35,32 @@ struct NttDomain {
 
 void ntt_domain_init(NttDomain& d, uint32_t log_n, hipStream_t st);
 
+constexpr int NTT_SM_LOG = 11;    // sub-transform twiddles: powers of omega_2048 (domain-independent)
+constexpr int NTT_TL_LOG = 12;    // omega_n^x = TL[x mod 4096] * TH[x / 4096]
+
+ZK_DI uint32_t bitrev32(uint32_t x, uint32_t log_n) {
+  return log_n ? (__builtin_bitreverse32(x) >> (32 - log_n)) : 0;
+}
+
+struct NttTabs {
+  const Fr* sm;   // omega_2048^j, j < 1024 (or the inverse root)
+  const Fr* tl;   // omega_n^x, x < min(n, 4096)
+  const Fr* th;   // omega_n^(4096 y), y < n / 4096
+};
+
+// omega_n^x, x < n
+ZK_DI Fr tw_full(const NttTabs& t, uint32_t x, uint32_t log_n) {
+  Fr w = ld_vec(&t.tl[x & ((1u << NTT_TL_LOG) - 1)]);
+  if (log_n > NTT_TL_LOG) w = fp_mul(w, ld_vec(&t.th[x >> NTT_TL_LOG]));
+  return w;
+}
+
+inline NttTabs tabs_of(const NttDomain& dom, bool inv) {
+  return inv ? NttTabs{dom.ism.as<Fr>(), dom.itl.as<Fr>(), dom.ith.as<Fr>()}
+             : NttTabs{dom.sm.as<Fr>(), dom.tl.as<Fr>(), dom.th.as<Fr>()};
+}
+
+
 // In-place passes over n Montgomery Fr.
 void ntt_dif(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st, Prof* pf = nullptr);
 void ntt_dit(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st, Prof* pf = nullptr);

@@ -20,6 +20,8 @@
 #include <thread>
 
 #include "ctx.hpp"
+#include "dist.hpp"
+#include "quotient.hpp"
 
 namespace zk {
 
@@ -54,27 +56,6 @@ void csr_upload(CsrDev& d, const zk_r1cs_csr* q, hipStream_t st) {
       ZK_HIP(hipStreamSynchronize(st));  // tmp dies here
     }
   }
-}
-
-struct CsrArgs {
-  const uint64_t* rp[3];
-  const uint32_t* col[3];
-  const Fr* val[3];
-};
-
-__device__ __forceinline__ Fr row_dot(const uint64_t* __restrict__ rp, const uint32_t* __restrict__ col,
-                                      const Fr* __restrict__ val, uint64_t row, const Fr* __restrict__ zc,
-                                      uint64_t V) {
-  Fr acc = fp_zero<FrParams>();
-  const uint64_t e = rp[row + 1];
-  for (uint64_t k = rp[row]; k < e; k++) {
-    const uint32_t c = col[k];
-    if (c >= V) continue;                   // qap:122-124
-    Fr zv = fp_to_mont(ld_vec(&zc[c]));
-    if (val) zv = fp_mul(zv, ld_vec(&val[k]));
-    acc = fp_add(acc, zv);
-  }
-  return acc;
 }
 
 // (Az)_j, (Bz)_j, (Cz)_j for every domain row (rows >= nc are zero padding,
@@ -131,12 +112,14 @@ __global__ void __launch_bounds__(256) k_h_final(const Fr* __restrict__ hb, cons
   hlo[i] = (uint64_t)h.v[0] | ((uint64_t)h.v[1] << 32);
 }
 
+// out[k] = low word of src[idx[k] / div] (div > 1: a distributed-quotient
+// rank holds H_(rank + div d) at position d)
 __global__ void __launch_bounds__(256) k_gather_lo64(const uint64_t* __restrict__ src, int stride_words,
-                                                     const uint32_t* __restrict__ idx, uint32_t count,
-                                                     uint64_t* __restrict__ out) {
+                                                     const uint32_t* __restrict__ idx, uint32_t div,
+                                                     uint32_t count, uint64_t* __restrict__ out) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= count) return;
-  out[k] = src[(size_t)idx[k] * stride_words];
+  out[k] = src[(size_t)(idx[k] / div) * stride_words];
 }
 
 struct Extras {
@@ -186,12 +169,15 @@ static void pow64_chain(const host::X<typename C::HF>& P, ABI* out) {
 }
 
 // Upload one base vector range [lo, hi): compact non-identity entries, append extras.
+// Positions lo, lo + stride, ... < hi (stride > 1: the H coefficients of a
+// shard, i = shard mod nshards, which is where the distributed quotient
+// leaves them).
 template <class C, class ABI>
 static void upload_vector(zk_pk_dev& pk, int slot, const ABI* v, uint64_t lo, uint64_t hi, uint64_t idx_offset,
-                          const std::vector<ABI>& extras, hipStream_t st) {
+                          const std::vector<ABI>& extras, hipStream_t st, uint64_t stride = 1) {
   std::vector<uint32_t> idx;
-  idx.reserve(hi - lo);
-  for (uint64_t i = lo; i < hi; i++)
+  idx.reserve((hi - lo) / stride + 1);
+  for (uint64_t i = lo; i < hi; i += stride)
     if (!v[i].infinity) idx.push_back((uint32_t)(i - lo));
   const uint32_t cnt = (uint32_t)idx.size();
   const uint32_t nex = (uint32_t)extras.size();
@@ -269,12 +255,10 @@ zk_pk_dev* pk_upload(zk_ctx* ctx, const zk_pk* pk, const zk_r1cs_csr* q, uint32_
     upload_vector<G1>(*d, MSM_IC, pk->ic_g1, lo, hi, pk->num_public + 1, none1, st);
   }
   {
-    // h_g1[i] pairs with H coefficient i (zip, core:211-215); H has n coefficients
+    // h_g1[i] pairs with H coefficient i (zip, core:211-215); H has n
+    // coefficients; shard k takes i = k mod nshards
     uint64_t L = std::min<uint64_t>(pk->h_len, d->n);
-    uint64_t lo = shard_lo(L, shard, nshards), hi = shard_lo(L, shard + 1, nshards);
-    d->h_lo = (uint32_t)lo;
-    d->h_hi = (uint32_t)hi;
-    upload_vector<G1>(*d, MSM_H, pk->h_g1, lo, hi, 0, none1, st);
+    upload_vector<G1>(*d, MSM_H, pk->h_g1, std::min<uint64_t>(shard, L), L, 0, none1, st, nshards);
   }
   // the a/b vectors may be shorter than V (core:171 `i < pk.a_g1.len()`): indices stay < V.
   pk_precompute_windows(ctx, *d);
@@ -359,8 +343,15 @@ static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipS
   pf->end(st, ph);
 }
 
+static bool dist_quotient_enabled() {
+  const char* e = getenv("ZK_DIST_QUOTIENT");
+  return !(e && std::strcmp(e, "0") == 0);
+}
+
+// h_given (virtual-rank tests): this shard's lo64(H_(shard + nshards d)) is
+// already on the device, with the witness-check flags of all ranks.
 static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, const zk_fr* r,
-                             const zk_fr* s) {
+                             const zk_fr* s, const uint64_t* h_given = nullptr, uint32_t given_flags = 0) {
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
   const auto t_start = clk::now();
@@ -375,17 +366,42 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   // Latency-bound phases (scan, bucket reduction) of one MSM overlap the
   // throughput-bound accumulation of another.
   ZK_HIP(hipEventRecord(ctx->ev_scal, st));           // z (and flags reset) ready
+  static const int sched = [] {
+    const char* e = getenv("ZK_PROVE_SCHED");
+    return e ? atoi(e) : 0;
+  }();
   auto stream_of = [&](int slot) {
+    if (sched == 3) return st;   // fully serial (per-phase profiling)
     return slot == MSM_H ? st : slot == MSM_B2 ? ctx->side[0] : slot == MSM_IC ? ctx->side[1] : ctx->side[2];
+  };
+  // The quotient: local (every coefficient), distributed over the RCCL
+  // ranks of a sharded key (this rank's coefficients i = shard mod N), or
+  // given (virtual-rank tests).
+  const bool dist = !h_given && pk->nshards > 1 && ctx->exch && ctx->exch->world == (int)pk->nshards &&
+                    ctx->exch->rank == (int)pk->shard && dist_quotient_ok(pk->n, (int)pk->nshards) &&
+                    dist_quotient_enabled();
+  const uint64_t* h_src = h_given ? h_given : ctx->tmp_scal.as<uint64_t>();
+  const uint32_t h_div = (h_given || dist) ? pk->nshards : 1;
+  auto run_quotient = [&]() {
+    if (h_given) return;
+    if (dist) {
+      ctx->tmp_scal.ensure(sizeof(uint64_t) * (pk->n / pk->nshards));
+      h_src = ctx->tmp_scal.as<uint64_t>();
+      dist_quotient(ctx, pk, d_z, *ctx->exch, ctx->dq, ctx->flags.as<uint32_t>(), ctx->tmp_scal.as<uint64_t>(), st);
+    } else {
+      quotient(ctx, pk, d_z, st);   // (Az, Bz, Cz) -> lo64(H) in tmp_scal
+      h_src = ctx->tmp_scal.as<uint64_t>();
+    }
   };
   auto launch_slot = [&](int slot) {
     hipStream_t ss = stream_of(slot);
     const uint32_t cnt = pk->count[slot], nex = pk->extras[slot];
     ctx->scal[slot].ensure(sizeof(uint64_t) * std::max<uint32_t>(cnt + nex, 1));
     if (cnt) {
-      const uint64_t* src = slot == MSM_H ? ctx->tmp_scal.as<uint64_t>() : d_z;
+      const uint64_t* src = slot == MSM_H ? h_src : d_z;
       const int stride = slot == MSM_H ? 1 : 4;
-      k_gather_lo64<<<ceil_div(cnt, 256), 256, 0, ss>>>(src, stride, pk->idx[slot].as<uint32_t>(), cnt,
+      k_gather_lo64<<<ceil_div(cnt, 256), 256, 0, ss>>>(src, stride, pk->idx[slot].as<uint32_t>(),
+                                                         slot == MSM_H ? h_div : 1u, cnt,
                                                          ctx->scal[slot].as<uint64_t>());
       ZK_LAUNCH_CHECK();
     }
@@ -415,12 +431,19 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       msm_download<G1>(ctx->msm[slot], ss);
     }
   };
+  // ZK_PROVE_SCHED=3: everything on the main stream, in order, with per-MSM
+  // phase names (profiling).  Default: the four independent MSMs start on
+  // the side streams, the quotient and then H on the main one.  (Holding the
+  // MSMs back until the quotient is done was measured slower: the quotient's
+  // latency-bound kernels leave most of the chip idle.)
+  static const char* const tags[NUM_MSM] = {"A/", "B2/", "B1/", "IC/", "H/"};
+  for (int slot = 0; slot < NUM_MSM; slot++) ctx->msm[slot].tag = sched == 3 ? tags[slot] : "";
   for (int k = 0; k < NUM_SIDE; k++) ZK_HIP(hipStreamWaitEvent(ctx->side[k], ctx->ev_scal, 0));
   for (int slot : {MSM_B2, MSM_IC, MSM_A, MSM_B1}) {
     launch_slot(slot);
     ZK_HIP(hipEventRecord(ctx->ev_done[slot], stream_of(slot)));
   }
-  quotient(ctx, pk, d_z, st);  // (Az, Bz, Cz) -> lo64(H) in tmp_scal, then H on the same stream
+  run_quotient();
   ctx->flags_host.ensure(16);
   ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
   launch_slot(MSM_H);
@@ -467,7 +490,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   ZK_HIP(hipStreamSynchronize(st));
   ctx->prof.add_host("host_finish", t_fin);
   ctx->prof.collect();
-  const uint32_t flags = *ctx->flags_host.as<uint32_t>();
+  const uint32_t flags = h_given ? given_flags : *ctx->flags_host.as<uint32_t>();
   p.status = ZK_OK;
   if (flags & 5u) p.status = ZK_ERR_INVALID_WITNESS;
   else if (flags & 2u) p.status = ZK_ERR_QAP_DIVISION;
@@ -475,6 +498,10 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
 }
 
 static int combine(const Partial* parts, size_t k, zk_proof* out) {
+  // the witness checks are spread over the ranks' rows: InvalidWitness
+  // (core:83-98, 124-128) wins over the division failure (qap:266)
+  for (size_t i = 0; i < k; i++)
+    if (parts[i].status == ZK_ERR_INVALID_WITNESS) return ZK_ERR_INVALID_WITNESS;
   for (size_t i = 0; i < k; i++)
     if (parts[i].status != ZK_OK) return parts[i].status;
   auto A = host::inf<host::Fq>(), C = A;
@@ -512,6 +539,56 @@ int prove_partial_impl(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, size_t
   }
   std::memcpy(out->bytes, &p, sizeof p);
   return p.status;
+}
+
+// N virtual ranks of a sharded key on ONE device: the distributed quotient's
+// stages run rank by rank, its three all-to-alls become device copies, then
+// each rank's MSMs and the fold.  Exercises exactly the per-rank code and
+// index maps the RCCL path runs (tests; the RCCL path needs N devices).
+int prove_virtual_shards_impl(zk_ctx* ctx, const zk_pk_dev* const* pks, uint32_t N, const void* d_z, size_t zlen,
+                              size_t num_public, const zk_fr* r, const zk_fr* s, zk_proof* out) {
+  if (N < 2) return ZK_ERR_ARG;
+  for (uint32_t k = 0; k < N; k++)
+    if (!pks[k] || pks[k]->shard != k || pks[k]->nshards != N || pks[k]->n != pks[0]->n) return ZK_ERR_ARG;
+  const zk_pk_dev* pk0 = pks[0];
+  if (num_public >= zlen || zlen != pk0->V) return ZK_ERR_INVALID_WITNESS;
+  if (!dist_quotient_ok(pk0->n, (int)N)) return ZK_ERR_ARG;
+  hipStream_t st = ctx->stream;
+  const uint64_t* z = reinterpret_cast<const uint64_t*>(d_z);
+  const uint64_t m = pk0->n / N;
+  std::vector<DistQ> dq(N);
+  std::vector<DevBuf> hb(N);
+  DevBuf flags;
+  flags.ensure(sizeof(uint32_t) * N);
+  ZK_HIP(hipMemsetAsync(flags.p, 0, sizeof(uint32_t) * N, st));
+  auto exchange = [&](int which) {
+    const size_t chunk = dq_chunk_bytes(pk0, (int)N, which);
+    for (uint32_t a = 0; a < N; a++)
+      for (uint32_t b = 0; b < N; b++) {
+        const DevBuf& src = which == 1 ? dq[b].s1 : which == 2 ? dq[b].s2 : dq[b].s3;
+        DevBuf& dst = which == 1 ? dq[a].r1 : which == 2 ? dq[a].r2 : dq[a].r3;
+        ZK_HIP(hipMemcpyAsync(static_cast<char*>(dst.p) + b * chunk, static_cast<const char*>(src.p) + a * chunk,
+                              chunk, hipMemcpyDeviceToDevice, st));
+      }
+  };
+  for (uint32_t k = 0; k < N; k++) dq_stage_a(ctx, pks[k], z, (int)k, (int)N, dq[k], flags.as<uint32_t>() + k, st);
+  exchange(1);
+  for (uint32_t k = 0; k < N; k++) dq_stage_b(ctx, pks[k], (int)k, (int)N, dq[k], st);
+  exchange(2);
+  for (uint32_t k = 0; k < N; k++) dq_stage_c(ctx, pks[k], (int)k, (int)N, dq[k], st);
+  exchange(3);
+  for (uint32_t k = 0; k < N; k++) {
+    hb[k].ensure(sizeof(uint64_t) * m);
+    dq_stage_d(ctx, pks[k], (int)k, (int)N, dq[k], hb[k].as<uint64_t>(), st);
+  }
+  std::vector<uint32_t> hf(N);
+  ZK_HIP(hipMemcpyAsync(hf.data(), flags.p, sizeof(uint32_t) * N, hipMemcpyDeviceToHost, st));
+  ZK_HIP(hipStreamSynchronize(st));
+  uint32_t all = 0;
+  for (uint32_t f : hf) all |= f;
+  std::vector<Partial> parts(N);
+  for (uint32_t k = 0; k < N; k++) parts[k] = prove_partial(ctx, pks[k], z, r, s, hb[k].as<uint64_t>(), all);
+  return combine(parts.data(), N, out);
 }
 
 int combine_impl(const zk_prove_partial* parts, size_t k, const zk_fr* r, const zk_fr* s, zk_proof* out) {

@@ -470,11 +470,15 @@ int setup_impl(zk_ctx* ctx, const zk_r1cs_csr* q, const zk_setup_params* P, uint
   ZK_HIP(hipMemcpyAsync(hh.data(), sh.p, 8 * n, hipMemcpyDeviceToHost, st));
   ZK_HIP(hipStreamSynchronize(st));
 
+  // contiguous shard ranges, or (stride = nshards) positions i = shard mod nshards
   auto build_slot = [&](int slot, bool g2, const std::vector<uint64_t>& hs, const DevBuf& ds, uint64_t len,
-                        uint64_t idx_offset, const std::vector<uint64_t>& extra_words, uint32_t nextra) {
-    const uint64_t lo = len * shard / nshards, hi = len * (shard + 1) / nshards;
+                        uint64_t idx_offset, const std::vector<uint64_t>& extra_words, uint32_t nextra,
+                        bool strided = false) {
+    const uint64_t lo = strided ? std::min<uint64_t>(shard, len) : len * shard / nshards;
+    const uint64_t hi = strided ? len : len * (shard + 1) / nshards;
+    const uint64_t stride = strided ? nshards : 1;
     std::vector<uint32_t> loc, glob;
-    for (uint64_t i = lo; i < hi; i++)
+    for (uint64_t i = lo; i < hi; i += stride)
       if (hs[i]) {
         loc.push_back((uint32_t)i);
         glob.push_back((uint32_t)(i + idx_offset));
@@ -535,9 +539,7 @@ int setup_impl(zk_ctx* ctx, const zk_r1cs_csr* q, const zk_setup_params* P, uint
   build_slot(MSM_B2, true, hb, sb, V, 0, exB2, nB2);
   build_slot(MSM_B1, false, hb, sb, V, 0, exB1, nB1);
   build_slot(MSM_IC, false, hic, sic, nic, num_public + 1, none, 0);
-  build_slot(MSM_H, false, hh, sh, n, 0, none, 0);
-  d->h_lo = (uint32_t)(n * shard / nshards);
-  d->h_hi = (uint32_t)(n * (shard + 1) / nshards);
+  build_slot(MSM_H, false, hh, sh, n, 0, none, 0, /*strided*/ true);
   pk_precompute_windows(ctx, *d);
   *pk_dev = d.release();
   return ZK_OK;

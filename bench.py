@@ -81,29 +81,41 @@ def phase_table(prof):
     return {k: {"ms": round(v["ms"], 3), "launches": v["launches"], "units": v["units"]} for k, v in prof.items()}
 
 
+# VALU view of the same kernel: every mixed add (madd-2008-s) in the prove's
+# G1 MSMs is 10 Fq multiplications of 14 x 14 radix-2^28 limb products plus
+# 14 x 14 for the Montgomery reduction = 3920 v_mad_u64_u32; a prove MSM has
+# 4 digit windows (64-bit scalars, c = 16).  Peak: tools/mulbench.hip, best
+# radix-2^28 variant, 72.2 G Fq-mul/s x 392 = 28.3 T v_mad_u64_u32/s.
+MADS_PER_MADD = 3920
+PROVE_WINDOWS = 4
+VALU_PEAK_TMADS = 28.3
+
+
 def roofline_from(prof):
+    """Dominant kernel: k_msm_accum<G1> (bucket accumulation of the four G1
+    MSMs), priced at SURVEY 8(d)'s 128 B per scalar-point pair."""
     g1 = prof.get("msm_accum_g1", {"ms": 0.0, "launches": 0, "units": 0})
-    g2 = prof.get("msm_accum_g2", {"ms": 0.0, "launches": 0, "units": 0})
-    ms = g1["ms"] + g2["ms"]
-    launches = g1["launches"] + g2["launches"]
+    ms, launches, units = g1["ms"], g1["launches"], g1["units"]
     if ms <= 0 or launches == 0:
         return None
-    algo_bytes = G1_PAIR_BYTES * g1["units"] + G2_PAIR_BYTES * g2["units"]
+    algo_bytes = G1_PAIR_BYTES * units
     achieved = algo_bytes / (ms / 1e3) / 1e9
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tpath):
         try:
-            t = json.load(open(tpath))
-            traffic = t.get("msm_accum_bytes_per_launch")
+            traffic = json.load(open(tpath)).get("msm_accum_g1_bytes_per_launch")
         except Exception:
             traffic = None
+    tmads = units * PROVE_WINDOWS * MADS_PER_MADD / (ms / 1e3) / 1e12
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-            "kernel": "k_msm_accum (G1+G2 bucket accumulation)",
+            "kernel": "k_msm_accum<G1>",
             "algorithmic_bytes_per_launch": int(algo_bytes / launches),
             "avg_launch_ms": round(ms / launches, 4),
-            "note": "VALU integer-multiply bound (381-bit Montgomery), not HBM; see DESIGN.md"}
+            "valu": {"achieved_tmad_per_s": round(tmads, 2), "peak_tmad_per_s": VALU_PEAK_TMADS,
+                     "frac": round(tmads / VALU_PEAK_TMADS, 4)},
+            "note": "integer-VALU bound (381-bit Montgomery products), not HBM; see DESIGN.md"}
 
 
 def cpu_baseline(zkp, ctx, log_n, seed):

@@ -2,6 +2,7 @@
 files committed under profiles/.
 
   python tools/prof_summary.py trace <run_results.db> <out.md>
+  python tools/prof_summary.py stats <run_kernel_stats.csv> <out.md>
   python tools/prof_summary.py pmc <fetch.db> <write.db> <out.json>
 
 PMC correction (MI355X_MICROARCH.md, HBM): on gfx950 FETCH_SIZE reports half
@@ -10,6 +11,7 @@ the bytes of wide coalesced reads, so traffic = 2*FETCH_SIZE + WRITE_SIZE
 calibrated access shape; the doubled figure is an upper estimate.
 """
 import json
+import re
 import sqlite3
 import sys
 
@@ -72,18 +74,43 @@ def pmc(fetch_db, write_db, out):
         wk = w.get(k, (0, 0.0))[1]
         kernels[k] = {"fetch_kib": round(fk, 1), "write_kib": round(wk, 1),
                       "traffic_bytes_per_launch": int((2 * fk + wk) * 1024)}
-    acc = [kernels[k] for k in kernels if k.startswith("k_msm_accum")]
-    res = {"note": "traffic = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch (gfx950 FETCH correction)",
+    res = {"note": "traffic = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch (gfx950 FETCH correction); "
+                   "averages over every dispatch of bench.py --no-msm (prove steps only)",
            "kernels": kernels}
-    if acc:
-        res["msm_accum_bytes_per_launch"] = int(sum(a["traffic_bytes_per_launch"] for a in acc) / len(acc))
+    for k in kernels:
+        if k.startswith("k_msm_accum"):
+            tag = "g2" if "G2" in k else "g1"
+            res[f"msm_accum_{tag}_bytes_per_launch"] = kernels[k]["traffic_bytes_per_launch"]
     json.dump(res, open(out, "w"), indent=1)
     for k, v in kernels.items():
         print(k, v)
 
 
+def stats(csv_path, out):
+    """rocprofv3 --stats CSV -> markdown table with short kernel names."""
+    import csv
+    rows = list(csv.DictReader(open(csv_path)))
+    lines = ["| kernel | calls | total ms | avg us | min us | max us | % |", "|---|---|---|---|---|---|---|"]
+    for r in rows:
+        name = r["Name"]
+        m = re.search(r"zk::(k_\w+)(<zk::(G1|G2)>|<(\w+)>)?", name)
+        if m:
+            short_name = m.group(1) + (f"<{m.group(3)}>" if m.group(3) else (f"<{m.group(4)}>" if m.group(4) else ""))
+        elif "rocprim" in name:
+            short_name = "rocprim radix_sort_onesweep " + ("histogram" if "histogram" in name else "iteration")
+        else:
+            short_name = name[:40]
+        lines.append(f"| {short_name} | {r['Calls']} | {int(r['TotalDurationNs']) / 1e6:.3f} | "
+                     f"{float(r['AverageNs']) / 1e3:.1f} | {int(r['MinNs']) / 1e3:.1f} | {int(r['MaxNs']) / 1e3:.1f} | "
+                     f"{float(r['Percentage']):.2f} |")
+    open(out, "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines[:12]))
+
+
 if __name__ == "__main__":
-    if sys.argv[1] == "trace":
+    if sys.argv[1] == "stats":
+        stats(sys.argv[2], sys.argv[3])
+    elif sys.argv[1] == "trace":
         trace(sys.argv[2], sys.argv[3])
     else:
         pmc(sys.argv[2], sys.argv[3], sys.argv[4])

@@ -244,16 +244,67 @@ ZK_DI bool fq2_is_zero(const Fq2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c
 ZK_DI Fq2 fq2_add(const Fq2& a, const Fq2& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
 ZK_DI Fq2 fq2_sub(const Fq2& a, const Fq2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
 ZK_DI Fq2 fq2_neg(const Fq2& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
-// sched_barrier between the three independent products keeps the scheduler
-// from interleaving them (3x the live 28-bit limb sets -> spills in G2).
+// Schoolbook product with lazy reduction: each output coefficient is ONE
+// product-scanning pass over two limb products and one Montgomery
+// reduction,
+//   c0 = REDC(a0 b0 - a1 b1 + 4p^2),   c1 = REDC(a0 b1 + a1 b0),
+// the same 1176 v_mad as Karatsuba's three full products but without its
+// five Fq additions / subtractions (12-limb carry chains, each link a VCC
+// hazard) and with two packs / final subtractions instead of three.  The
+// subtracted products go through v_mad_i64_i32 on negated 28-bit limbs; the
+// 4p^2 column offset keeps the total non-negative (a1 b1 < 4 p^2 for inputs
+// < 2p), so signed column sums and arithmetic carries give a value < 2p.
+template <bool SUB>
+ZK_DI Fq fq_redc2(const uint32_t (&x0)[14], const uint32_t (&y0)[14], const uint32_t (&x1)[14],
+                  const uint32_t (&y1)[14]) {
+  constexpr int M = 14;
+  uint32_t m[M], r[M];
+  int32_t nx1[M];
+#pragma unroll
+  for (int i = 0; i < M; i++) nx1[i] = SUB ? -(int32_t)x1[i] : (int32_t)x1[i];
+  int64_t carry = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * M - 1; k++) {
+    int64_t acc = carry;
+    if (SUB) acc += (int64_t)FqParams::P4SQ28[k];
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < M) {
+        acc += (int64_t)((uint64_t)x0[i] * y0[j]);
+        acc += (int64_t)nx1[i] * (int64_t)(int32_t)y1[j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < M) acc += (int64_t)((uint64_t)m[i] * FqParams::MOD28[j]);
+    }
+    if (k < M) {
+      m[k] = ((uint32_t)acc * FqParams::INV28) & 0x0fffffffu;
+      acc += (int64_t)((uint64_t)m[k] * FqParams::MOD28[0]);
+    } else {
+      r[k - M] = (uint32_t)acc & 0x0fffffffu;
+    }
+    carry = acc >> 28;   // arithmetic: floor division of a possibly negative column
+  }
+  r[M - 1] = (uint32_t)(carry + (SUB ? (int64_t)FqParams::P4SQ28[2 * M - 1] : 0));
+  Fq o;
+  pack28<12, M>(r, o.v);
+  return fp_reduce_once(o);
+}
+
 ZK_DI Fq2 fq2_mul(const Fq2& a, const Fq2& b) {
-  Fq t0 = fq_mul(a.c0, b.c0);
+  uint32_t a0[14], a1[14], b0[14], b1[14];
+  unpack28<12, 14>(a.c0.v, a0);
+  unpack28<12, 14>(a.c1.v, a1);
+  unpack28<12, 14>(b.c0.v, b0);
+  unpack28<12, 14>(b.c1.v, b1);
+  Fq c0 = fq_redc2<true>(a0, b0, a1, b1);
   __builtin_amdgcn_sched_barrier(0);
-  Fq t1 = fq_mul(a.c1, b.c1);
+  Fq c1 = fq_redc2<false>(a0, b1, a1, b0);
   __builtin_amdgcn_sched_barrier(0);
-  Fq m = fq_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
-  __builtin_amdgcn_sched_barrier(0);
-  return {fp_sub(t0, t1), fp_sub(fp_sub(m, t0), t1)};
+  return {c0, c1};
 }
 ZK_DI Fq2 fq2_sqr(const Fq2& a) {
   // (c0 + c1 u)^2 = (c0+c1)(c0-c1) + 2 c0 c1 u

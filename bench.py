@@ -188,6 +188,36 @@ def msm_g1_bench(zkp, ctx, log_n, steps, warmup, seed):
     return {"pairs_per_s": round(n / dt, 1), "n": n, "scalar_bits": 255, "ms_per_msm": round(dt * 1e3, 3)}
 
 
+def ntt_bench(zkp, ctx, log_n, steps, warmup, seed):
+    """configs[2]: forward radix-2 NTT over Fr, 2^log_n points in HBM, plus a
+    round-trip check (inverse of the forward is the identity)."""
+    import ctypes as C
+    import torch
+    n = 1 << log_n
+    x = random_fr(np.random.default_rng(seed), n)
+    d = torch.from_numpy(x.view(np.int64).copy()).to(f"cuda:{ctx.device}")
+    L = zkp.lib()
+    h = C.c_void_p(ctx._h)
+
+    def run(direction):
+        zkp._check(L.zk_ntt_fr_dev(h, C.c_void_p(d.data_ptr()), C.c_uint32(log_n), C.c_int(direction), None),
+                   ctx, "zk_ntt_fr_dev")
+    for _ in range(warmup):
+        run(1)
+        run(-1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run(1)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    for _ in range(steps):
+        run(-1)
+    ok = bool(np.array_equal(d.cpu().numpy().view(np.uint64).reshape(-1, 4), x))
+    return {"log_n": log_n, "ms_per_ntt": round(dt * 1e3, 3), "elements_per_s": round(n / dt, 1),
+            "roundtrip_identity": ok}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -282,6 +312,8 @@ def main():
         if not args.no_msm:
             log("[bench] G1 MSM 2^20 (configs[1])")
             extra["msm_g1"] = msm_g1_bench(zkp, ctx, 20, args.steps, args.warmup, args.seed + 11)
+            log("[bench] NTT 2^22 (configs[2])")
+            extra["ntt"] = ntt_bench(zkp, ctx, 22, args.steps, args.warmup, args.seed + 31)
         if not args.no_cpu_baseline:
             log(f"[bench] CPU baseline: oracle prove at 2^{args.cpu_log_n}, 1 thread")
             extra["cpu_baseline"] = cpu_baseline(zkp, ctx, args.cpu_log_n, args.seed + 21)

@@ -304,8 +304,27 @@ __global__ void __launch_bounds__(128) k_msm_accum(const typename C::A* __restri
   X acc;
   xyzz_set_inf(acc);
   uint32_t cur = key[start], run_start = start;
+  // Optional software pipeline (C::PREFETCH): the next entry's base is
+  // loaded into registers before this entry's addition, its sign applied
+  // only at use.  Off for both groups: G1's 3 waves/SIMD hide the gathers,
+  // and for G2 it measured no better than the plain loop.
+  uint32_t ent_nx = ent[start];
+  typename C::A nx = ld_vec(&bases[ent_nx & 0x7fffffffu]);
   for (uint32_t e = start; e < end; e++) {
     const uint32_t g = key[e];
+    typename C::A a;
+    uint32_t en;
+    if (C::PREFETCH) {
+      a = nx;
+      en = ent_nx;
+      if (e + 1 < end) {
+        ent_nx = ent[e + 1];
+        nx = ld_vec(&bases[ent_nx & 0x7fffffffu]);
+      }
+    } else {
+      en = ent[e];
+      a = ld_vec(&bases[en & 0x7fffffffu]);
+    }
     if (g != cur) {
       const bool head = (run_start == start) && (off[cur] < start);
       if (head) st_vec(&partials[2 * (size_t)t], acc);
@@ -314,7 +333,7 @@ __global__ void __launch_bounds__(128) k_msm_accum(const typename C::A* __restri
       cur = g;
       run_start = e;
     }
-    typename C::A a = load_point<C>(bases, ent[e]);
+    if (en & 0x80000000u) a.y = f_neg(a.y);
     if (!aff_is_inf(a)) acc = xyzz_madd(acc, a);
   }
   const bool head = (run_start == start) && (off[cur] < start);

@@ -250,7 +250,10 @@ def main():
         # travels over the torch process group
         obj = [zkp.Context.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        ctx.attach_rccl(obj[0], rank, world)
+        try:
+            ctx.attach_rccl(obj[0], rank, world)
+        except zkp.GrothError as e:   # every rank then recomputes the whole quotient
+            log(f"[bench] RCCL attach failed ({e}); quotient replicated per rank")
     n = (1 << args.log_n) * world
     log_n_total = n.bit_length() - 1
     params, r, s = setup_params(args.seed)

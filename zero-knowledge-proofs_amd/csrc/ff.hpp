@@ -186,8 +186,43 @@ ZK_DI Fp<P> fp_mul(const Fp<P>& a, const Fp<P>& b) {
   pack28<N, M>(r, o.v);
   return fp_reduce_once(o);
 }
+// Squaring: column k of a^2 is 2 sum_{i<j} a_i a_j (+ a_{k/2}^2), so the
+// product half needs M(M+1)/2 v_mad instead of M^2 (Fq: 105 vs 196); the
+// interleaved Montgomery reduction is unchanged.
 template <class P>
-ZK_DI Fp<P> fp_sqr(const Fp<P>& a) { return fp_mul(a, a); }
+ZK_DI Fp<P> fp_sqr(const Fp<P>& a) {
+  constexpr int N = P::N, M = P::N28;
+  uint32_t x[M], m[M], r[M];
+  unpack28<N, M>(a.v, x);
+  uint64_t carry = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * M - 1; k++) {
+    uint64_t cross = 0;
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+      const int j = k - i;
+      if (i < j && j < M) cross += (uint64_t)x[i] * x[j];
+    }
+    uint64_t acc = carry + (cross << 1);
+    if ((k & 1) == 0 && k / 2 < M) acc += (uint64_t)x[k / 2] * x[k / 2];
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < M) acc += (uint64_t)m[i] * P::MOD28[j];
+    }
+    if (k < M) {
+      m[k] = ((uint32_t)acc * P::INV28) & 0x0fffffffu;
+      acc += (uint64_t)m[k] * P::MOD28[0];
+    } else {
+      r[k - M] = (uint32_t)acc & 0x0fffffffu;
+    }
+    carry = acc >> 28;
+  }
+  r[M - 1] = (uint32_t)carry;
+  Fp<P> o;
+  pack28<N, M>(r, o.v);
+  return fp_reduce_once(o);
+}
 
 template <class P>
 ZK_DI Fp<P> fp_to_mont(const Fp<P>& canon) { return fp_mul(canon, fp_from_const<P>(P::R2)); }
@@ -324,7 +359,7 @@ ZK_DI Fq2 fq2_inv(const Fq2& a) {
 ZK_DI Fq f_add(const Fq& a, const Fq& b) { return fp_add(a, b); }
 ZK_DI Fq f_sub(const Fq& a, const Fq& b) { return fp_sub(a, b); }
 ZK_DI Fq f_mul(const Fq& a, const Fq& b) { return fq_mul(a, b); }
-ZK_DI Fq f_sqr(const Fq& a) { return fq_mul(a, a); }
+ZK_DI Fq f_sqr(const Fq& a) { return fp_sqr(a); }
 ZK_DI Fq f_neg(const Fq& a) { return fp_neg(a); }
 ZK_DI bool f_is_zero(const Fq& a) { return fp_is_zero(a); }
 ZK_DI Fq f_inv(const Fq& a) { return fq_inv(a); }

@@ -545,9 +545,9 @@ static uint32_t accum_threads() {
     ZK_HIP(hipGetDevice(&dev));
     ZK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_accum<C>, 128, 0));
-    int rounds = 1;
-    if (const char* e = getenv("ZK_MSM_ROUNDS")) rounds = std::max(1, atoi(e));
-    return (uint32_t)std::max(1, per_cu * cus * 128 * rounds);
+    double rounds = 1.0;   // tuning: fractions leave room for concurrent streams
+    if (const char* e = getenv("ZK_MSM_ROUNDS")) rounds = std::max(0.05, atof(e));
+    return (uint32_t)std::max(1.0, per_cu * cus * 128 * rounds);
   }();
   return T;
 }

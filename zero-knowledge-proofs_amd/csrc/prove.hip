@@ -433,9 +433,11 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   };
   // ZK_PROVE_SCHED=3: everything on the main stream, in order, with per-MSM
   // phase names (profiling).  Default: the four independent MSMs start on
-  // the side streams, the quotient and then H on the main one.  (Holding the
-  // MSMs back until the quotient is done was measured slower: the quotient's
-  // latency-bound kernels leave most of the chip idle.)
+  // the side streams, the quotient and then H on the main one.  Measured
+  // alternatives (11.4 ms default): MSMs held until the quotient is done
+  // 12.1 ms; accumulate launches sized to 1/2, 3/4 or 2 rounds of the chip
+  // (leaving room for the quotient) 12.8 / 12.1 / 12.7 ms; quotient enqueued
+  // before the side MSMs: within noise.
   static const char* const tags[NUM_MSM] = {"A/", "B2/", "B1/", "IC/", "H/"};
   for (int slot = 0; slot < NUM_MSM; slot++) ctx->msm[slot].tag = sched == 3 ? tags[slot] : "";
   for (int k = 0; k < NUM_SIDE; k++) ZK_HIP(hipStreamWaitEvent(ctx->side[k], ctx->ev_scal, 0));

@@ -153,3 +153,19 @@ def test_rccl_attach_single_rank(zkp):
     assert len(uid) == 128
     with zkp.Context(0) as c:
         c.attach_rccl(uid, 0, 1)
+
+
+def test_prove_all_ones_witness(ctx, zkp, oracle):
+    """x = y = z = 1 in every row: every MSM scalar is 0 or 1 and H = 0, so
+    the shared-bucket MSMs see dummy entries for all zero digits and one
+    giant bucket (the merge path); the proof must still match the oracle."""
+    qap, csr_o, params, r, s, _ = _synthetic(zkp, oracle, 10, 4242)
+    n = 1 << 10
+    z = np.zeros((3 * n + 1, 4), dtype=np.uint64)
+    z[:, 0] = 1
+    rc, opk, _ = oracle.setup(csr_o, params, 1, nthreads=8)
+    rc, oproof = oracle.prove(opk, csr_o, z, 1, r, s)
+    assert rc == 0
+    pk = U.pk_from_oracle(zkp, opk, qap, 1)
+    dpk = pk.upload(ctx)
+    assert np.array_equal(zkp.Prover.prove(dpk, zkp.Witness(z, 1), r=r, s=s).words, oproof)

@@ -156,6 +156,8 @@ __global__ void __launch_bounds__(256) k_msm_digits(const uint64_t* __restrict__
   }
 }
 
+constexpr uint32_t MSM_DUMMY = 0x7fffffffu;   // entry that contributes nothing
+
 // Radix-sort path: one (bucket, entry) pair per (point, window), written
 // window-major (coalesced); a zero digit gets the key G, which sorts after
 // every bucket, so off[G] still counts the non-zero digits.
@@ -184,8 +186,15 @@ __global__ void __launch_bounds__(256) k_msm_keys(const uint64_t* __restrict__ s
       carry = 0;
     }
     const size_t o = (size_t)w * p.n + i;
-    key[o] = mag ? (p.shared ? 0u : p.boff[w]) + mag - 1 : p.G;
-    ent[o] = (p.shared ? (uint32_t)o : i) | (neg ? 0x80000000u : 0u);   // shared: base 2^(c w) P_i at w n + i
+    if (p.shared) {
+      // shared buckets: keys stay < G = 2^16 (two 8-bit radix passes) -- a
+      // zero digit becomes a dummy entry of bucket 0 that adds nothing
+      key[o] = mag ? mag - 1 : 0u;
+      ent[o] = mag ? ((uint32_t)o | (neg ? 0x80000000u : 0u)) : MSM_DUMMY;   // base 2^(c w) P_i at w n + i
+    } else {
+      key[o] = mag ? p.boff[w] + mag - 1 : p.G;
+      ent[o] = i | (neg ? 0x80000000u : 0u);
+    }
   }
 }
 
@@ -269,14 +278,8 @@ __global__ void __launch_bounds__(256) k_scan_down(uint32_t* __restrict__ counts
 }
 
 // --------------------------------------------------------- accumulate ---
-template <class C>
-__device__ __forceinline__ typename C::A load_point(const typename C::A* __restrict__ bases, uint32_t e) {
-  typename C::A a = ld_vec(&bases[e & 0x7fffffffu]);
-  if (e & 0x80000000u) a.y = f_neg(a.y);
-  return a;
-}
 
-// Chunk length: the M non-zero digits (known on device only) split evenly
+// Chunk length: the M grouped entries (known on device only) split evenly
 // over the T accumulate threads, T = one full-occupancy wave set of the
 // chip, so every launch is exactly one balanced round whatever the digit
 // distribution.
@@ -296,7 +299,7 @@ __global__ void __launch_bounds__(128) k_msm_accum(const typename C::A* __restri
                                                    typename C::X* __restrict__ partials) {
   using X = typename C::X;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t M = off[G];  // non-zero digits (known on device only)
+  const uint32_t M = off[G];  // grouped entries (known on device only)
   const uint32_t K = chunk_len(M, T);
   const uint32_t start = t * K;
   if (t >= T || start >= M) return;
@@ -304,27 +307,9 @@ __global__ void __launch_bounds__(128) k_msm_accum(const typename C::A* __restri
   X acc;
   xyzz_set_inf(acc);
   uint32_t cur = key[start], run_start = start;
-  // Optional software pipeline (C::PREFETCH): the next entry's base is
-  // loaded into registers before this entry's addition, its sign applied
-  // only at use.  Off for both groups: G1's 3 waves/SIMD hide the gathers,
-  // and for G2 it measured no better than the plain loop.
-  uint32_t ent_nx = ent[start];
-  typename C::A nx = ld_vec(&bases[ent_nx & 0x7fffffffu]);
   for (uint32_t e = start; e < end; e++) {
     const uint32_t g = key[e];
-    typename C::A a;
-    uint32_t en;
-    if (C::PREFETCH) {
-      a = nx;
-      en = ent_nx;
-      if (e + 1 < end) {
-        ent_nx = ent[e + 1];
-        nx = ld_vec(&bases[ent_nx & 0x7fffffffu]);
-      }
-    } else {
-      en = ent[e];
-      a = ld_vec(&bases[en & 0x7fffffffu]);
-    }
+    const uint32_t en = ent[e];
     if (g != cur) {
       const bool head = (run_start == start) && (off[cur] < start);
       if (head) st_vec(&partials[2 * (size_t)t], acc);
@@ -333,6 +318,8 @@ __global__ void __launch_bounds__(128) k_msm_accum(const typename C::A* __restri
       cur = g;
       run_start = e;
     }
+    if (en == MSM_DUMMY) continue;   // zero digit (shared-bucket plans)
+    typename C::A a = ld_vec(&bases[en & 0x7fffffffu]);
     if (en & 0x80000000u) a.y = f_neg(a.y);
     if (!aff_is_inf(a)) acc = xyzz_madd(acc, a);
   }
@@ -577,9 +564,9 @@ static void msm_launch_impl(MsmWork& w, const typename C::A* d_bases, const uint
   const bool g2 = sizeof(typename C::A) == sizeof(G2A);
   int ph = pf ? pf->begin(st, (w.tag + "msm_sort").c_str(), n) : -1;   // group (point, window) entries by bucket
   if (msm_sort_mode() == 0 || p.shared) {
-    // rocPRIM radix sort on ceil(log2(G + 1)) key bits
+    // rocPRIM radix sort on ceil(log2(G + 1)) key bits (log2(G) when shared)
     unsigned end_bit = 1;
-    while ((1ull << end_bit) <= p.G) end_bit++;
+    while ((1ull << end_bit) < (uint64_t)p.G + (p.shared ? 0 : 1)) end_bit++;
     w.key_in.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
     w.ent_in.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
     size_t tmp_bytes = 0;
@@ -679,7 +666,7 @@ template <class C>
 void msm_launch_shared(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scalars, int sw, uint32_t n,
                        int bits, int c, hipStream_t st) {
   w.plan = msm_make_plan_shared(n, bits, sw, c);
-  if ((uint64_t)n * w.plan.nwin >= 0x80000000ull) throw Error(ZK_ERR_ARG, "msm: too many window bases");
+  if ((uint64_t)n * w.plan.nwin >= MSM_DUMMY) throw Error(ZK_ERR_ARG, "msm: too many window bases");
   msm_launch_impl<C>(w, d_bases, d_scalars, sw, n, st);
 }
 

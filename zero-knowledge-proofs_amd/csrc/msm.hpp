@@ -40,7 +40,6 @@ struct G1 {
   using X = G1X;
   using HF = host::Fq;
   static constexpr int ABI_WORDS = 13;  // zk_g1_affine
-  static constexpr bool PREFETCH = false;   // 3 waves/SIMD already hide the gathers
 };
 struct G2 {
   using F = Fq2;
@@ -48,7 +47,6 @@ struct G2 {
   using X = G2X;
   using HF = host::Fq2;
   static constexpr int ABI_WORDS = 25;  // zk_g2_affine
-  static constexpr bool PREFETCH = false;   // measured: no gain at 1 wave/SIMD (2.50 vs 2.58 ms)
 };
 
 constexpr int MSM_MAXWIN = 64;

@@ -353,7 +353,7 @@ __device__ __forceinline__ bool big_bucket(const uint32_t* off, uint32_t b, uint
 
 template <class C>
 __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ off, uint32_t G, uint32_t T, uint32_t fix_max,
-                                                   typename C::X* __restrict__ buckets,
+                                                   uint32_t* __restrict__ nbig, typename C::X* __restrict__ buckets,
                                                    const typename C::X* __restrict__ partials) {
   using X = typename C::X;
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -362,7 +362,11 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
   const uint32_t bs = off[g], be = off[g + 1];
   if (be == bs) return;
   const uint32_t t0 = bs / K, t1 = (be - 1) / K;
-  if (t0 == t1 || t1 - t0 + 1 > fix_max) return;
+  if (t0 == t1) return;
+  if (t1 - t0 + 1 > fix_max) {   // left to the merge levels, which skip themselves when none exist
+    atomicAdd(nbig, 1u);
+    return;
+  }
   X acc = ld_vec(&partials[2 * (size_t)t0 + 1]);
   for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, ld_vec(&partials[2 * (size_t)t]));
   st_vec(&buckets[g], acc);
@@ -371,15 +375,16 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
 template <class C>
 __global__ void __launch_bounds__(128) k_msm_merge(const uint32_t* __restrict__ key,
                                                    const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
-                                                   uint32_t fix_max, uint32_t level,
+                                                   uint32_t fix_max, uint32_t level, const uint32_t* __restrict__ nbig,
                                                    typename C::X* __restrict__ buckets,
                                                    const typename C::X* __restrict__ in,
                                                    typename C::X* __restrict__ out) {
   using X = typename C::X;
-  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (*nbig == 0) return;   // no bucket over fix_max chunks: nothing at any level
   const uint32_t M = off[G];
   const uint32_t K = chunk_len(M, T);
   const uint64_t W = (uint64_t)K << (2 * level);   // MSM_MERGE_FAN = 4
+  for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;; u += gridDim.x * blockDim.x) {
   const uint64_t s64 = (uint64_t)u * W;
   if (s64 >= M) return;
   const uint32_t s = (uint32_t)s64, e = (uint32_t)min<uint64_t>(s64 + W, M);
@@ -408,6 +413,7 @@ __global__ void __launch_bounds__(128) k_msm_merge(const uint32_t* __restrict__ 
     if (off[b] >= s && off[b + 1] <= e) st_vec(&buckets[b], acc);   // complete
     else if (off[b] < s) st_vec(&out[2 * (size_t)u], acc);           // open at the start
     else st_vec(&out[2 * (size_t)u + 1], acc);                       // open at the end
+  }
   }
 }
 
@@ -630,8 +636,10 @@ static void msm_launch_impl(MsmWork& w, const typename C::A* d_bases, const uint
     if (pf) pf->end(st, ph);
   }
   ph = pf ? pf->begin(st, (w.tag + "msm_merge").c_str(), p.G) : -1;   // buckets split across chunks
-  k_msm_fixup<C><<<ceil_div(p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), p.G, p.T, p.fix_max, w.buckets.as<X>(),
-                                                      w.partials.as<X>());
+  w.nbig.ensure(sizeof(uint32_t));
+  ZK_HIP(hipMemsetAsync(w.nbig.p, 0, sizeof(uint32_t), st));
+  k_msm_fixup<C><<<ceil_div(p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), p.G, p.T, p.fix_max,
+                                                      w.nbig.as<uint32_t>(), w.buckets.as<X>(), w.partials.as<X>());
   ZK_LAUNCH_CHECK();
   {
     X* a = w.partials.as<X>();
@@ -639,8 +647,11 @@ static void msm_launch_impl(MsmWork& w, const typename C::A* d_bases, const uint
     // level l merges groups of 4^l chunks; T chunks at most
     for (uint32_t level = 1; (1ull << (2 * (level - 1))) < p.T; level++) {
       const uint32_t groups = (uint32_t)(((uint64_t)p.T + (1ull << (2 * level)) - 1) >> (2 * level));
-      k_msm_merge<C><<<ceil_div(groups, 128), 128, 0, st>>>(w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T,
-                                                             p.fix_max, level, w.buckets.as<X>(), a, b);
+      // a small grid-stride grid: the common case exits at once and should
+      // not queue hundreds of blocks behind other streams' long kernels
+      k_msm_merge<C><<<std::min<uint32_t>(ceil_div(groups, 128), 64), 128, 0, st>>>(
+          w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T, p.fix_max, level, w.nbig.as<uint32_t>(),
+          w.buckets.as<X>(), a, b);
       ZK_LAUNCH_CHECK();
       std::swap(a, b);
     }

@@ -79,6 +79,7 @@ MsmPlan msm_make_plan_shared(uint32_t n, int bits, int sw, int c);
 struct MsmWork {
   DevBuf counts, off, cursor, scan_part, ent, key, buckets, partials, partials2, rc, res;
   DevBuf key_in, ent_in, sort_tmp;   // radix-sort path
+  DevBuf nbig;                       // buckets left to the merge levels
   PinnedBuf host_res;
   MsmPlan plan{};
   Prof* prof = nullptr;  // optional live kernel timing

@@ -57,6 +57,8 @@ MsmPlan msm_make_plan(uint32_t n, int bits, int sw, int force_c) {
   p.nq = q;
   p.nred = p.nwin;
   p.shared = 0;
+  p.nseg = 1;
+  p.segshift = 31;
   return p;
 }
 
@@ -80,6 +82,32 @@ MsmPlan msm_make_plan_shared(uint32_t n, int bits, int sw, int c) {
   p.rcoff[1] = p.nrc = (1u << p.kr[0]) + (1u << p.kc[0]);
   p.qoff[0] = 0;
   p.qoff[1] = p.nq = p.kr[0] + p.kc[0] + 1;
+  p.nseg = 1;
+  p.segshift = 31;
+  return p;
+}
+
+// Batch plan: segment k = one MSM with its own 2^k buckets [k 2^k, (k+1) 2^k)
+// and its own reduction window.
+static MsmPlan msm_make_plan_batch(const MsmSeg* segs, int nseg, int bits, int c) {
+  uint32_t total = 0;
+  for (int k = 0; k < nseg; k++) total += segs[k].n;
+  MsmPlan p = msm_make_plan_shared(total, bits, 1, c);
+  const int kb = p.kr[0] + p.kc[0];
+  p.nseg = nseg;
+  p.nred = nseg;
+  p.segshift = kb;
+  for (int k = 0; k < nseg; k++) {
+    p.nb[k] = 1u << kb;
+    p.kr[k] = p.kr[0];
+    p.kc[k] = p.kc[0];
+    p.boff[k] = (uint32_t)k << kb;
+    p.rcoff[k] = k * ((1u << p.kr[0]) + (1u << p.kc[0]));
+    p.qoff[k] = k * (p.kr[0] + p.kc[0] + 1);
+  }
+  p.boff[nseg] = p.G = (uint32_t)nseg << kb;
+  p.rcoff[nseg] = p.nrc = nseg * ((1u << p.kr[0]) + (1u << p.kc[0]));
+  p.qoff[nseg] = p.nq = nseg * (p.kr[0] + p.kc[0] + 1);
   return p;
 }
 
@@ -161,11 +189,14 @@ constexpr uint32_t MSM_DUMMY = 0x7fffffffu;   // entry that contributes nothing
 // Radix-sort path: one (bucket, entry) pair per (point, window), written
 // window-major (coalesced); a zero digit gets the key G, which sorts after
 // every bucket, so off[G] still counts the non-zero digits.
+// Batches call it once per MSM with that MSM's n, its first bucket key_base
+// and key / ent advanced to its first entry.
 template <int SW>
-__global__ void __launch_bounds__(256) k_msm_keys(const uint64_t* __restrict__ sc, MsmPlan p,
-                                                  uint32_t* __restrict__ key, uint32_t* __restrict__ ent) {
+__global__ void __launch_bounds__(256) k_msm_keys(const uint64_t* __restrict__ sc, MsmPlan p, uint32_t n,
+                                                  uint32_t key_base, uint32_t* __restrict__ key,
+                                                  uint32_t* __restrict__ ent) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= p.n) return;
+  if (i >= n) return;
   uint64_t s[SW];
 #pragma unroll
   for (int k = 0; k < SW; k++) s[k] = sc[(size_t)i * SW + k];
@@ -185,11 +216,12 @@ __global__ void __launch_bounds__(256) k_msm_keys(const uint64_t* __restrict__ s
       mag = v;
       carry = 0;
     }
-    const size_t o = (size_t)w * p.n + i;
+    const size_t o = (size_t)w * n + i;
     if (p.shared) {
-      // shared buckets: keys stay < G = 2^16 (two 8-bit radix passes) -- a
-      // zero digit becomes a dummy entry of bucket 0 that adds nothing
-      key[o] = mag ? mag - 1 : 0u;
+      // shared buckets: keys stay < 2^16 per MSM (two 8-bit radix passes
+      // for one) -- a zero digit becomes a dummy entry of the MSM's bucket 0
+      // that adds nothing
+      key[o] = key_base + (mag ? mag - 1 : 0u);
       ent[o] = mag ? ((uint32_t)o | (neg ? 0x80000000u : 0u)) : MSM_DUMMY;   // base 2^(c w) P_i at w n + i
     } else {
       key[o] = mag ? p.boff[w] + mag - 1 : p.G;
@@ -290,8 +322,13 @@ __device__ __forceinline__ uint32_t chunk_len(uint32_t M, uint32_t T) { return M
 //   complete bucket                        -> buckets[g]
 //   run begun by an earlier thread (head)   -> partials[2t]
 //   run continued by a later thread (tail)  -> partials[2t+1]
+template <class A>
+struct SegBases {
+  const A* p[MSM_MAXSEG];
+};
+
 template <class C>
-__global__ void __launch_bounds__(128) k_msm_accum(const typename C::A* __restrict__ bases,
+__global__ void __launch_bounds__(128) k_msm_accum(SegBases<typename C::A> sb, uint32_t segshift, uint32_t idx_mask,
                                                    const uint32_t* __restrict__ ent,
                                                    const uint32_t* __restrict__ key,
                                                    const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
@@ -319,7 +356,12 @@ __global__ void __launch_bounds__(128) k_msm_accum(const typename C::A* __restri
       run_start = e;
     }
     if (en == MSM_DUMMY) continue;   // zero digit (shared-bucket plans)
-    typename C::A a = ld_vec(&bases[en & 0x7fffffffu]);
+    const uint32_t seg = g >> segshift;   // batch: the MSM owning bucket g
+    const typename C::A* bases = sb.p[0];
+#pragma unroll
+    for (int k = 1; k < MSM_MAXSEG; k++)
+      if (seg == (uint32_t)k) bases = sb.p[k];
+    typename C::A a = ld_vec(&bases[en & idx_mask]);
     if (en & 0x80000000u) a.y = f_neg(a.y);
     if (!aff_is_inf(a)) acc = xyzz_madd(acc, a);
   }
@@ -545,14 +587,19 @@ static uint32_t accum_threads() {
   return T;
 }
 
+// One MSM (nseg = 1) or a batch of MSMs sharing every phase: segment k's
+// keys start at bucket k << segshift and its entries at sum_{j<k} nwin n_j.
 template <class C>
-static void msm_launch_impl(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scalars, int sw,
-                            uint32_t n, hipStream_t st) {
+static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hipStream_t st) {
   using X = typename C::X;
   MsmPlan& p = w.plan;
   if (p.G > (uint32_t)MSM_SCAN_BLOCK * 1024) throw Error(ZK_ERR_ARG, "msm: too many buckets");
-  const size_t M = (size_t)n * p.nwin;
+  if (nseg < 1 || nseg > MSM_MAXSEG || (nseg > 1 && (!p.shared || sw != 1)))
+    throw Error(ZK_ERR_ARG, "msm: bad batch");
+  size_t M = 0;
+  for (int k = 0; k < nseg; k++) M += (size_t)segs[k].n * p.nwin;
   if (M >= 0x80000000ull) throw Error(ZK_ERR_ARG, "msm: too many (point, window) entries");
+  const uint32_t n = p.n;   // all points of the batch (profiling units)
   const uint32_t nblk = ceil_div(p.G, MSM_SCAN_BLOCK);
   w.off.ensure(sizeof(uint32_t) * (p.G + 1));
   w.ent.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
@@ -565,6 +612,8 @@ static void msm_launch_impl(MsmWork& w, const typename C::A* d_bases, const uint
   w.partials2.ensure(sizeof(X) * ((size_t)p.T / 2 + 2));
   w.rc.ensure(sizeof(X) * p.nrc);
   w.res.ensure(sizeof(X) * p.nq);
+  SegBases<typename C::A> sb{};
+  for (int k = 0; k < nseg; k++) sb.p[k] = static_cast<const typename C::A*>(segs[k].bases);
 
   Prof* pf = w.prof;
   const bool g2 = sizeof(typename C::A) == sizeof(G2A);
@@ -578,20 +627,27 @@ static void msm_launch_impl(MsmWork& w, const typename C::A* d_bases, const uint
     size_t tmp_bytes = 0;
     sort_pairs_u32(nullptr, tmp_bytes, nullptr, nullptr, nullptr, nullptr, M, end_bit, st);
     w.sort_tmp.ensure(tmp_bytes);
-    if (n) {
-      const uint32_t nb = ceil_div(n, 256);
-      if (sw == 1)
-        k_msm_keys<1><<<nb, 256, 0, st>>>(d_scalars, p, w.key_in.as<uint32_t>(), w.ent_in.as<uint32_t>());
-      else
-        k_msm_keys<4><<<nb, 256, 0, st>>>(d_scalars, p, w.key_in.as<uint32_t>(), w.ent_in.as<uint32_t>());
+    size_t eoff = 0;
+    for (int k = 0; k < nseg; k++) {
+      const uint32_t nk = segs[k].n;
+      if (!nk) continue;
+      const uint32_t nb = ceil_div(nk, 256);
+      const uint32_t kbase = p.shared ? (uint32_t)k << (p.segshift & 31) : 0u;
+      uint32_t* ki = w.key_in.as<uint32_t>() + eoff;
+      uint32_t* ei = w.ent_in.as<uint32_t>() + eoff;
+      if (sw == 1) k_msm_keys<1><<<nb, 256, 0, st>>>(segs[k].scalars, p, nk, nseg > 1 ? kbase : 0u, ki, ei);
+      else k_msm_keys<4><<<nb, 256, 0, st>>>(segs[k].scalars, p, nk, 0u, ki, ei);
       ZK_LAUNCH_CHECK();
+      eoff += (size_t)nk * p.nwin;
+    }
+    if (M)
       sort_pairs_u32(w.sort_tmp.p, tmp_bytes, w.key_in.as<uint32_t>(), w.key.as<uint32_t>(),
                      w.ent_in.as<uint32_t>(), w.ent.as<uint32_t>(), M, end_bit, st);
-    }
     k_msm_offsets<<<ceil_div(M + 1, 256), 256, 0, st>>>(w.key.as<uint32_t>(), (uint32_t)M, p.G, w.off.as<uint32_t>());
     ZK_LAUNCH_CHECK();
   } else {
-    // counting sort: global-atomic histogram, scan, scatter
+    // counting sort: global-atomic histogram, scan, scatter (single MSM)
+    const uint64_t* d_scalars = segs[0].scalars;
     if (w.counts.bytes < sizeof(uint32_t) * (p.G + 1)) {   // zero once; k_scan_down re-zeroes
       w.counts.ensure(sizeof(uint32_t) * (p.G + 1));
       ZK_HIP(hipMemsetAsync(w.counts.p, 0, w.counts.bytes, st));
@@ -629,9 +685,15 @@ static void msm_launch_impl(MsmWork& w, const typename C::A* d_bases, const uint
   // accumulate threads split it evenly there (chunk_len), no host sync.
   if (M) {
     ph = pf ? pf->begin(st, (w.tag + (g2 ? "msm_accum_g2" : "msm_accum_g1")).c_str(), n) : -1;
-    k_msm_accum<C><<<ceil_div(p.T, 128), 128, 0, st>>>(d_bases, w.ent.as<uint32_t>(), w.key.as<uint32_t>(),
-                                                        w.off.as<uint32_t>(), p.G, p.T, w.buckets.as<X>(),
-                                                        w.partials.as<X>());
+    // ZK_MSM_IDXMASK (experiment only, wrong results): confine the base
+    // gathers to a cache-resident prefix to measure the kernel without HBM
+    static const uint32_t idx_mask = [] {
+      const char* e = getenv("ZK_MSM_IDXMASK");
+      return e ? (uint32_t)strtoul(e, nullptr, 0) & 0x7fffffffu : 0x7fffffffu;
+    }();
+    k_msm_accum<C><<<ceil_div(p.T, 128), 128, 0, st>>>(sb, p.segshift, idx_mask, w.ent.as<uint32_t>(),
+                                                        w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T,
+                                                        w.buckets.as<X>(), w.partials.as<X>());
     ZK_LAUNCH_CHECK();
     if (pf) pf->end(st, ph);
   }
@@ -670,7 +732,8 @@ template <class C>
 void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scalars, int sw, uint32_t n,
                 int bits, hipStream_t st) {
   w.plan = msm_make_plan(n, bits, sw);
-  msm_launch_impl<C>(w, d_bases, d_scalars, sw, n, st);
+  const MsmSeg seg{d_bases, d_scalars, n};
+  msm_launch_impl<C>(w, &seg, 1, sw, st);
 }
 
 template <class C>
@@ -678,7 +741,17 @@ void msm_launch_shared(MsmWork& w, const typename C::A* d_bases, const uint64_t*
                        int bits, int c, hipStream_t st) {
   w.plan = msm_make_plan_shared(n, bits, sw, c);
   if ((uint64_t)n * w.plan.nwin >= MSM_DUMMY) throw Error(ZK_ERR_ARG, "msm: too many window bases");
-  msm_launch_impl<C>(w, d_bases, d_scalars, sw, n, st);
+  const MsmSeg seg{d_bases, d_scalars, n};
+  msm_launch_impl<C>(w, &seg, 1, sw, st);
+}
+
+template <class C>
+void msm_launch_batch(MsmWork& w, const MsmSeg* segs, int nseg, int bits, int c, hipStream_t st) {
+  if (nseg < 1 || nseg > MSM_MAXSEG) throw Error(ZK_ERR_ARG, "msm: batch of 1..4 MSMs");
+  w.plan = msm_make_plan_batch(segs, nseg, bits, c);
+  for (int k = 0; k < nseg; k++)
+    if ((uint64_t)segs[k].n * w.plan.nwin >= MSM_DUMMY) throw Error(ZK_ERR_ARG, "msm: too many window bases");
+  msm_launch_impl<C>(w, segs, nseg, 1, st);
 }
 
 // ------------------------------------------- precomputed window bases -----
@@ -768,21 +841,25 @@ void msm_download(MsmWork& w, hipStream_t st) {
 // Every quantity is a point times a power of two:
 //   U^C_b : 2^(c w + kc + b),  U^D_b : 2^(c w + b),  P : 2^(c w)
 // so one Horner pass over exponents from the top combines everything.
+// seg < 0: every reduction window (one MSM); seg = k: window k alone (MSM k
+// of a batch, weight 1).
 template <class C>
-host::X<typename C::HF> msm_finish(const MsmWork& w) {
+static host::X<typename C::HF> msm_finish_impl(const MsmWork& w, int seg) {
   using HF = typename C::HF;
   using HX = host::X<HF>;
   static_assert(sizeof(HX) == sizeof(typename C::X), "layout");
   const MsmPlan& p = w.plan;
   const HX* r = w.host_res.as<const HX>();
   // reduction window `win` carries weight 2^(c win); a shared plan has one
-  // window of weight 1 (the shifts live in the precomputed bases)
+  // window of weight 1 (the shifts live in the precomputed bases), a batch
+  // one window of weight 1 per MSM
   auto wexp = [&](int win) { return p.shared ? 0 : p.c * win; };
+  const int w0 = seg < 0 ? 0 : seg, w1 = seg < 0 ? (int)p.nred : seg + 1;
   int maxe = 0;
-  for (int win = 0; win < (int)p.nred; win++)
+  for (int win = w0; win < w1; win++)
     maxe = std::max(maxe, wexp(win) + std::max<int>(p.kc[win] + p.kr[win] - 1, p.kc[win]));
   std::vector<std::vector<const HX*>> at(maxe + 1);
-  for (int win = 0; win < (int)p.nred; win++) {
+  for (int win = w0; win < w1; win++) {
     const int kr = p.kr[win], kc = p.kc[win];
     for (int q = 0; q < kr + kc + 1; q++) {
       int e = q < kr ? wexp(win) + kc + q : q < kr + kc ? wexp(win) + (q - kr) : wexp(win);
@@ -798,6 +875,18 @@ host::X<typename C::HF> msm_finish(const MsmWork& w) {
     for (const HX* t : at[e]) acc = host::addp(acc, host_form(*t));
   }
   return acc;
+}
+
+template <class C>
+host::X<typename C::HF> msm_finish(const MsmWork& w) {
+  if (w.plan.nseg > 1) throw Error(ZK_ERR_ARG, "msm: batch results are per segment");
+  return msm_finish_impl<C>(w, -1);
+}
+
+template <class C>
+host::X<typename C::HF> msm_finish_seg(const MsmWork& w, int seg) {
+  if (seg < 0 || seg >= w.plan.nseg) throw Error(ZK_ERR_ARG, "msm: no such batch segment");
+  return msm_finish_impl<C>(w, seg);
 }
 
 // --------------------------------------------------- base conversion -----
@@ -879,6 +968,8 @@ void host_to_abi<G2>(const host::X<host::Fq2>& p, uint64_t* w) {
   template void batch_normalize<C>(const C::X*, size_t, C::F*, C::A*, hipStream_t);                    \
   template void msm_download<C>(MsmWork&, hipStream_t);                                              \
   template host::X<C::HF> msm_finish<C>(const MsmWork&);                                            \
+  template host::X<C::HF> msm_finish_seg<C>(const MsmWork&, int);                                   \
+  template void msm_launch_batch<C>(MsmWork&, const MsmSeg*, int, int, int, hipStream_t);            \
   template void convert_bases<C>(const uint64_t*, C::A*, size_t, hipStream_t);                       \
   template void convert_bases_gather<C>(const uint64_t*, const uint32_t*, C::A*, size_t, hipStream_t);
 ZK_MSM_INST(G1)

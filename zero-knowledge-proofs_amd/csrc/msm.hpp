@@ -64,8 +64,19 @@ struct MsmPlan {
   uint8_t kr[MSM_MAXWIN], kc[MSM_MAXWIN];   // nb = 2^(kr + kc): rows x columns
   uint32_t rcoff[MSM_MAXWIN + 1];   // first row/col sum of window w (rows, then columns)
   uint32_t qoff[MSM_MAXWIN + 1];    // first quantity of window w (U^C, U^D, P)
-  uint32_t nred;                    // reduction windows (nwin, or 1 when shared)
+  uint32_t nred;                    // reduction windows (nwin, or 1 when shared, or nseg)
   int shared;                       // windows share one bucket set (precomputed 2^(c w) P bases)
+  int nseg;                         // batch: independent MSMs, reduction window k = MSM k
+  uint32_t segshift;                // batch: bucket g belongs to MSM g >> segshift
+};
+
+// One MSM of a batch (msm_launch_batch): n points, window-shifted bases
+// (nwin x n, window-major) and n one-word scalars.
+constexpr int MSM_MAXSEG = 4;
+struct MsmSeg {
+  const void* bases;
+  const uint64_t* scalars;
+  uint32_t n;
 };
 
 MsmPlan msm_make_plan(uint32_t n, int bits, int sw, int force_c = 0);
@@ -95,6 +106,13 @@ void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scal
 template <class C>
 void msm_launch_shared(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scalars, int sw,
                        uint32_t n, int bits, int c, hipStream_t st);
+// Up to MSM_MAXSEG independent MSMs over window-shifted bases with 64-bit
+// scalars, run as ONE key pass / sort / accumulate / merge / bucket
+// reduction: MSM k owns buckets [k 2^s, (k+1) 2^s).  The latency-bound
+// phases (merge, row/column sums, quantities) then cost one tree depth for
+// the whole batch instead of one per MSM.  msm_finish_seg(w, k) gives MSM k.
+template <class C>
+void msm_launch_batch(MsmWork& w, const MsmSeg* segs, int nseg, int bits, int c, hipStream_t st);
 // d_bases[w n + i] = 2^(c w) d_bases[i] for 0 < w < W (the first n are given;
 // capacity W n).  One-time, at proving-key upload.
 template <class C>
@@ -110,6 +128,9 @@ void msm_download(MsmWork& w, hipStream_t st);
 // Host tail: combine the window partials into sum k_i P_i (host XYZZ).
 template <class C>
 host::X<typename C::HF> msm_finish(const MsmWork& w);
+// Host tail of MSM `seg` of a batch.
+template <class C>
+host::X<typename C::HF> msm_finish_seg(const MsmWork& w, int seg);
 
 // canonical ABI points -> device Montgomery affine ((0,0) = infinity)
 template <class C>

@@ -393,8 +393,9 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       h_src = ctx->tmp_scal.as<uint64_t>();
     }
   };
-  auto launch_slot = [&](int slot) {
-    hipStream_t ss = stream_of(slot);
+  // scalars of one MSM: lo64 of its variables (or H coefficients), then the
+  // extras' scalars (1 for alpha_1 / beta_2 / beta_1, the u64 limbs of r or s)
+  auto prep_scalars = [&](int slot, hipStream_t ss) {
     const uint32_t cnt = pk->count[slot], nex = pk->extras[slot];
     ctx->scal[slot].ensure(sizeof(uint64_t) * std::max<uint32_t>(cnt + nex, 1));
     if (cnt) {
@@ -406,7 +407,6 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       ZK_LAUNCH_CHECK();
     }
     if (nex) {
-      // scalar 1 for alpha_1 / beta_2 / beta_1, then the four u64 limbs of r (or s)
       Extras ex{};
       ex.v[0] = 1;
       const zk_fr* full = slot == MSM_A ? r : slot == MSM_B2 ? s : nullptr;
@@ -414,7 +414,10 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       k_set_extras<<<1, 64, 0, ss>>>(ctx->scal[slot].as<uint64_t>() + cnt, ex, nex);
       ZK_LAUNCH_CHECK();
     }
-    const uint32_t n = cnt + nex;
+  };
+  auto launch_slot = [&](int slot, hipStream_t ss) {
+    prep_scalars(slot, ss);
+    const uint32_t n = pk->count[slot] + pk->extras[slot];
     if (slot == MSM_B2) {
       if (pk->win > 1)
         msm_launch_shared<G2>(ctx->msm[slot], pk->bases[slot].as<G2A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64,
@@ -431,55 +434,154 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       msm_download<G1>(ctx->msm[slot], ss);
     }
   };
-  // ZK_PROVE_SCHED=3: everything on the main stream, in order, with per-MSM
-  // phase names (profiling).  Default: the four independent MSMs start on
-  // the side streams, the quotient and then H on the main one.  Measured
-  // alternatives (11.4 ms default): MSMs held until the quotient is done
-  // 12.1 ms; accumulate launches sized to 1/2, 3/4 or 2 rounds of the chip
-  // (leaving room for the quotient) 12.8 / 12.1 / 12.7 ms; quotient enqueued
-  // before the side MSMs: within noise.
   static const char* const tags[NUM_MSM] = {"A/", "B2/", "B1/", "IC/", "H/"};
   for (int slot = 0; slot < NUM_MSM; slot++) ctx->msm[slot].tag = sched == 3 ? tags[slot] : "";
-  for (int k = 0; k < NUM_SIDE; k++) ZK_HIP(hipStreamWaitEvent(ctx->side[k], ctx->ev_scal, 0));
-  for (int slot : {MSM_B2, MSM_IC, MSM_A, MSM_B1}) {
-    launch_slot(slot);
-    ZK_HIP(hipEventRecord(ctx->ev_done[slot], stream_of(slot)));
-  }
-  run_quotient();
-  ctx->flags_host.ensure(16);
-  ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
-  launch_slot(MSM_H);
-  ZK_HIP(hipEventRecord(ctx->ev_done[MSM_H], st));
-  if (ph_span >= 0) {
-    for (int slot : {MSM_B2, MSM_IC, MSM_A, MSM_B1}) ZK_HIP(hipStreamWaitEvent(st, ctx->ev_done[slot], 0));
-    ctx->prof.end(st, ph_span);
+  // Batched G1 (default with window-shifted keys): the G1 MSMs run in groups,
+  // each group ONE msm_launch_batch (one sort, accumulate, merge and bucket
+  // reduction, so the latency-bound tails cost one tree depth per group) in
+  // the workspace of its first slot.  ZK_G1_GROUPS lists the groups, letters
+  // A (pi_A), B (B_1), I (IC), H (H), comma-separated; default "ABI,H": A, B1
+  // and IC start on side[1] with the witness, H follows the quotient on the
+  // main stream, the G2 MSM runs on side[0].  ZK_PROVE_SCHED: 0 G2 starts
+  // with the witness, 1 G2 waits for the quotient, 3 everything serial on
+  // main.  ZK_MSM_BATCH=0 keeps one MSM per slot on four streams (below).
+  static const bool batch_env = [] {
+    const char* e = getenv("ZK_MSM_BATCH");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  static const std::vector<std::vector<int>> groups = [] {
+    const char* e = getenv("ZK_G1_GROUPS");
+    std::string spec = e ? e : "ABI,H";
+    std::vector<std::vector<int>> g(1);
+    for (char ch : spec) {
+      if (ch == ',') { if (!g.back().empty()) g.emplace_back(); continue; }
+      const int slot = ch == 'A' ? MSM_A : ch == 'B' ? MSM_B1 : ch == 'I' ? MSM_IC : ch == 'H' ? MSM_H : -1;
+      if (slot >= 0) g.back().push_back(slot);
+    }
+    if (g.back().empty()) g.pop_back();
+    int seen = 0;
+    for (auto& grp : g) for (int sl : grp) seen |= 1 << sl;
+    if (seen != ((1 << MSM_A) | (1 << MSM_B1) | (1 << MSM_IC) | (1 << MSM_H)))
+      g = {{MSM_A, MSM_B1, MSM_IC}, {MSM_H}};
+    return g;
+  }();
+  const bool batch = batch_env && pk->win > 1;
+  std::vector<int> waits;   // slots whose ev_done the host tail waits for
+  if (batch) {
+    hipStream_t s2 = sched == 3 ? st : ctx->side[0];
+    auto launch_group = [&](const std::vector<int>& grp, hipStream_t gs) {
+      MsmSeg segs[MSM_MAXSEG];
+      for (size_t k = 0; k < grp.size(); k++) {
+        const int slot = grp[k];
+        prep_scalars(slot, gs);
+        segs[k] = MsmSeg{pk->bases[slot].p, ctx->scal[slot].as<uint64_t>(), pk->count[slot] + pk->extras[slot]};
+      }
+      MsmWork& w = ctx->msm[grp[0]];
+      if (sched == 3) {
+        w.tag.clear();
+        for (int sl : grp) w.tag += tags[sl][0];
+        w.tag += "/";
+      }
+      msm_launch_batch<G1>(w, segs, (int)grp.size(), 64, pk->win_c, gs);
+      msm_download<G1>(w, gs);
+      ZK_HIP(hipEventRecord(ctx->ev_done[grp[0]], gs));
+      waits.push_back(grp[0]);
+    };
+    auto has_h = [](const std::vector<int>& grp) { return std::find(grp.begin(), grp.end(), (int)MSM_H) != grp.end(); };
+    if (sched == 3) {
+      launch_slot(MSM_B2, st);
+    } else if (sched != 1) {
+      ZK_HIP(hipStreamWaitEvent(s2, ctx->ev_scal, 0));
+      launch_slot(MSM_B2, s2);
+    }
+    // groups without H start with the witness on side[1], side[2], ...
+    int side = 1;
+    std::vector<hipStream_t> used;
+    for (const auto& grp : groups) {
+      if (has_h(grp)) continue;
+      hipStream_t gs = st;
+      if (sched != 3) {
+        gs = ctx->side[side];
+        side = side + 1 < NUM_SIDE ? side + 1 : 1;
+        ZK_HIP(hipStreamWaitEvent(gs, ctx->ev_scal, 0));
+        used.push_back(gs);
+      }
+      launch_group(grp, gs);
+    }
+    run_quotient();
+    if (sched == 1) {
+      ZK_HIP(hipEventRecord(ctx->ev_quot, st));
+      ZK_HIP(hipStreamWaitEvent(s2, ctx->ev_quot, 0));
+      launch_slot(MSM_B2, s2);
+    }
+    ZK_HIP(hipEventRecord(ctx->ev_done[MSM_B2], s2));
+    waits.push_back(MSM_B2);
+    ctx->flags_host.ensure(16);
+    ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
+    for (const auto& grp : groups)
+      if (has_h(grp)) launch_group(grp, st);
+    if (ph_span >= 0) {
+      for (int sl : waits) ZK_HIP(hipStreamWaitEvent(st, ctx->ev_done[sl], 0));
+      ctx->prof.end(st, ph_span);
+    }
+  } else {
+    // ZK_PROVE_SCHED=3: everything on the main stream, in order, with per-MSM
+    // phase names.  Default: the four independent MSMs start on the side
+    // streams, the quotient and then H on the main one.
+    for (int k = 0; k < NUM_SIDE; k++) ZK_HIP(hipStreamWaitEvent(ctx->side[k], ctx->ev_scal, 0));
+    for (int slot : {MSM_B2, MSM_IC, MSM_A, MSM_B1}) {
+      launch_slot(slot, stream_of(slot));
+      ZK_HIP(hipEventRecord(ctx->ev_done[slot], stream_of(slot)));
+    }
+    run_quotient();
+    ctx->flags_host.ensure(16);
+    ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
+    launch_slot(MSM_H, st);
+    ZK_HIP(hipEventRecord(ctx->ev_done[MSM_H], st));
+    waits = {MSM_A, MSM_B2, MSM_B1, MSM_IC, MSM_H};
+    if (ph_span >= 0) {
+      for (int slot : {MSM_B2, MSM_IC, MSM_A, MSM_B1}) ZK_HIP(hipStreamWaitEvent(st, ctx->ev_done[slot], 0));
+      ctx->prof.end(st, ph_span);
+    }
   }
 
-  // Host tails (Horner over each MSM's window partials, then s A + r B1) run
-  // as each MSM's stream reaches its event, overlapping the MSMs still on
-  // the GPU -- the H MSM, queued behind the quotient, usually finishes last.
+  // Host tails (Horner over each MSM's partials, then s A + r B1) run as
+  // each MSM's stream reaches its event, overlapping the MSMs still on the
+  // GPU.
   ctx->prof.add_host("host_launch", ms_since(t_start));
   double t_fin = 0;
   Partial p{};
-  bool done[NUM_MSM] = {}, sc_done = false;
-  for (int left = NUM_MSM; left > 0;) {
+  std::vector<bool> done(waits.size(), false);
+  bool sc_done = false, a_done = false, b1_done = false;
+  for (size_t left = waits.size(); left > 0;) {
     bool progressed = false;
-    for (int slot = 0; slot < NUM_MSM; slot++) {
-      if (done[slot]) continue;
+    for (size_t wi = 0; wi < waits.size(); wi++) {
+      if (done[wi]) continue;
+      const int slot = waits[wi];
       const hipError_t q = hipEventQuery(ctx->ev_done[slot]);
       if (q == hipErrorNotReady) continue;
       ZK_HIP(q);
       const auto t_f = clk::now();
-      switch (slot) {
-        case MSM_A: p.A = msm_finish<G1>(ctx->msm[slot]); break;
-        case MSM_B2: p.B2 = msm_finish<G2>(ctx->msm[slot]); break;
-        case MSM_B1: p.B1 = msm_finish<G1>(ctx->msm[slot]); break;
-        case MSM_IC: p.IC = msm_finish<G1>(ctx->msm[slot]); break;
-        case MSM_H: p.H = msm_finish<G1>(ctx->msm[slot]); break;
+      auto take = [&](int sl, const host::X<host::Fq>& v) {
+        switch (sl) {
+          case MSM_A: p.A = v; a_done = true; break;
+          case MSM_B1: p.B1 = v; b1_done = true; break;
+          case MSM_IC: p.IC = v; break;
+          case MSM_H: p.H = v; break;
+        }
+      };
+      if (slot == MSM_B2) {
+        p.B2 = msm_finish<G2>(ctx->msm[slot]);
+      } else if (batch) {
+        for (const auto& grp : groups)
+          if (grp[0] == slot)
+            for (size_t k = 0; k < grp.size(); k++) take(grp[k], msm_finish_seg<G1>(ctx->msm[slot], (int)k));
+      } else {
+        take(slot, msm_finish<G1>(ctx->msm[slot]));
       }
-      done[slot] = progressed = true;
+      done[wi] = progressed = true;
       left--;
-      if (!sc_done && done[MSM_A] && done[MSM_B1]) {
+      if (!sc_done && a_done && b1_done) {
         p.SC = host::mul2_scalar(p.A, s->l, p.B1, r->l);
         sc_done = true;
       }

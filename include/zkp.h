@@ -215,6 +215,31 @@ int zk_test_prove_virtual_shards(zk_ctx *ctx, const zk_pk_dev *const *shards, ui
 /* ark-serialize CanonicalSerialize, compressed (zcash flag bits), for
  * Proof (crates/groth16-core/src/lib.rs:28): a(48) | b(96) | c(48). */
 int zk_proof_serialize_compressed(const zk_proof *proof, uint8_t out[192]);
+/* CanonicalDeserialize, compressed, with ark's Validate::Yes checks: the
+ * compression flag, infinity without the sort flag, x < p, a point on the
+ * curve with the flagged root, in the prime-order subgroup.  Anything else
+ * -> ZK_ERR_ARG (ark's SerializationError). */
+int zk_proof_deserialize_compressed(const uint8_t in[192], zk_proof *out);
+
+/* -------------------------------------------------------------- verify --- */
+/* Host-only (no GPU): a handful of sequential pairings per call. */
+/* Verifier::verify (crates/groth16-core/src/lib.rs:308-355): *valid = 1 iff
+ * e(A,B) e(-alpha,beta) e(-IC,gamma) e(-C,delta) == 1 with
+ * IC = ic_g1[0] + sum_i lo64(public_inputs[i]) ic_g1[i+1] (core:322-338).
+ * n_inputs != vk->num_public -> ZK_ERR_INVALID_WITNESS (core:315-320).  The
+ * reference's own proofs fail this check unless every derived setup scalar is
+ * below 2^64 (lo64 truncation) -- mirrored, not fixed. */
+int zk_groth16_verify(const zk_vk *vk, const zk_proof *proof, const zk_fr *public_inputs,
+                      size_t n_inputs, int *valid);
+/* BatchVerifier::verify_batch (core:360-432) with its Fr::rand coefficients
+ * made explicit (coeffs[k] for proof k, canonical): ONE pairing check on
+ * sum c_k A_k, sum c_k B_k, sum c_k IC_k, sum c_k C_k -- the reference's rule
+ * as written.  n_proofs == 0 -> *valid = 1. */
+int zk_groth16_verify_batch(const zk_vk *vk, const zk_proof *proofs, const zk_fr *const *public_inputs,
+                            const size_t *n_inputs, size_t n_proofs, const zk_fr *coeffs, int *valid);
+/* prod_i e(g1[i], g2[i]) == 1 -> *result = 1 (Bls12_381::multi_pairing(..)
+ * .is_zero(), core:352).  Points must be canonical and on their curves. */
+int zk_pairing_product_is_one(const zk_g1_affine *g1, const zk_g2_affine *g2, size_t n, int *result);
 
 #ifdef __cplusplus
 }

@@ -169,3 +169,25 @@ def test_prove_all_ones_witness(ctx, zkp, oracle):
     pk = U.pk_from_oracle(zkp, opk, qap, 1)
     dpk = pk.upload(ctx)
     assert np.array_equal(zkp.Prover.prove(dpk, zkp.Witness(z, 1), r=r, s=s).words, oproof)
+
+
+def test_gpu_proof_verifies_when_untruncated(ctx, zkp):
+    """The reference's test_simple_proof (core:445-481) end to end on the GPU:
+    GPU setup with parameters whose derived scalars stay below 2^64 (so the
+    lo64 truncation is the identity), GPU prove, host Verifier::verify.
+    Full-width parameters give a proof the verifier rejects, as the
+    reference's does."""
+    cs = zkp.R1CS(0)
+    x, y, z = (cs.allocate_variable() for _ in range(3))
+    cs.enforce_multiplication(zkp.LinearCombination.from_variable(x), zkp.LinearCombination.from_variable(y),
+                              zkp.LinearCombination.from_variable(z))
+    qap = zkp.QAP.from_r1cs(cs)
+    w = zkp.Witness([1, 3, 4, 12], 1)
+    for params, ok in (((2, 3, 1, 1, 5), True), ((0x1234567890ABCDEF1234567890, 7, 11, 13, 17), False)):
+        crs = zkp.CRS.generate_from_qap(ctx, qap, zkp.SetupParams(*params), 1)
+        dpk = crs.pk.upload(ctx)
+        proof = zkp.Prover.prove(dpk, w, r=0xABCDEF, s=0x123456789)
+        assert zkp.Verifier.verify(crs.vk, proof, [3]) is ok
+        assert not zkp.Verifier.verify(crs.vk, proof, [5])
+        assert zkp.Proof.deserialize_compressed(proof.serialize_compressed()) == proof
+        dpk.free()

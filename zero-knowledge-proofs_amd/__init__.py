@@ -9,6 +9,7 @@ argument meaning and error behaviour follow the reference crates:
   QAP.from_r1cs / degree               crates/groth16-qap/src/lib.rs:95-187, 285-294
   SetupParams / CRS.generate_from_qap  crates/groth16-setup/src/lib.rs:82-278
   Witness / Prover.prove / Proof       crates/groth16-core/src/lib.rs:27-272
+  Verifier / BatchVerifier             crates/groth16-core/src/lib.rs:303-432
   GrothError kinds                     crates/groth16-core/src/lib.rs:47-77
 
 There is no CPU fallback: every compute call goes through libzkp_amd.so on a
@@ -41,7 +42,8 @@ EXPORTS = (
     "zk_groth16_prove", "zk_groth16_prove_dev", "zk_pk_upload_shard",
     "zk_groth16_setup_dev_shard", "zk_groth16_prove_partial", "zk_groth16_prove_combine",
     "zk_proof_serialize_compressed", "zk_rccl_unique_id", "zk_ctx_attach_rccl",
-    "zk_test_prove_virtual_shards",
+    "zk_test_prove_virtual_shards", "zk_proof_deserialize_compressed", "zk_groth16_verify",
+    "zk_groth16_verify_batch", "zk_pairing_product_is_one",
 )
 
 
@@ -493,6 +495,21 @@ class VerificationKey:
         self.num_public = num_public
         self.s = _VK()
         self.s.ic_g1 = self.ic_g1.ctypes.data
+        self.s.ic_len = num_public + 1
+        self.s.num_public = num_public
+
+    @classmethod
+    def from_points(cls, alpha_g1, beta_g2, gamma_g2, delta_g2, ic_g1):
+        """Build from canonical affine words (13 per G1, 25 per G2 point)."""
+        ic = np.asarray(ic_g1, dtype=np.uint64).reshape(-1, G1_WORDS)
+        vk = cls(len(ic) - 1)
+        vk.ic_g1[:] = ic
+        for name, words in (("alpha_g1", alpha_g1), ("beta_g2", beta_g2), ("gamma_g2", gamma_g2),
+                            ("delta_g2", delta_g2)):
+            field = getattr(vk.s, name)
+            for i, w in enumerate(np.asarray(words, dtype=np.uint64).reshape(-1)):
+                field.w[i] = int(w)
+        return vk
 
     def point(self, name):
         return np.array(getattr(self.s, name).w, dtype=np.uint64)
@@ -611,6 +628,17 @@ class Proof:
         _check(lib().zk_proof_serialize_compressed(C.byref(self._c()), out), None, "serialize")
         return bytes(out)
 
+    @classmethod
+    def deserialize_compressed(cls, data):
+        """ark CanonicalDeserialize (compressed, validated); ValueError on bad bytes."""
+        data = bytes(data)
+        if len(data) != 192:
+            raise ValueError("a compressed Proof is 192 bytes")
+        buf = (C.c_uint8 * 192).from_buffer_copy(data)
+        out = _Proof()
+        _check(lib().zk_proof_deserialize_compressed(buf, C.byref(out)), None, "deserialize")
+        return cls._from_c(out)
+
     def __eq__(self, other):
         return isinstance(other, Proof) and np.array_equal(self.words, other.words)
 
@@ -679,3 +707,59 @@ class Prover:
                                             C.byref(out))
         _check(rc, None, "zk_groth16_prove_combine")
         return Proof._from_c(out)
+
+
+# ------------------------------------------------------------- verify ----
+def _fr_rows(values):
+    a = values if isinstance(values, np.ndarray) else fr_array(values)
+    return np.ascontiguousarray(a, dtype=np.uint64).reshape(-1, 4)
+
+
+def pairing_product_is_one(g1_points, g2_points):
+    """prod e(P_i, Q_i) == 1 (Bls12_381::multi_pairing(..).is_zero(), core:352)."""
+    a = np.ascontiguousarray(g1_points, dtype=np.uint64).reshape(-1, G1_WORDS)
+    b = np.ascontiguousarray(g2_points, dtype=np.uint64).reshape(-1, G2_WORDS)
+    if len(a) != len(b):
+        raise ValueError("as many G1 as G2 points")
+    out = C.c_int(0)
+    _check(lib().zk_pairing_product_is_one(_p(a), _p(b), C.c_size_t(len(a)), C.byref(out)), None, "pairing")
+    return bool(out.value)
+
+
+class Verifier:
+    """Verifier::verify (crates/groth16-core/src/lib.rs:308-355), on the host."""
+
+    @staticmethod
+    def verify(vk, proof, public_inputs):
+        inp = _fr_rows(public_inputs)
+        valid = C.c_int(0)
+        rc = lib().zk_groth16_verify(C.byref(vk.s), C.byref(proof._c()), _p(inp) if len(inp) else None,
+                                     C.c_size_t(len(inp)), C.byref(valid))
+        _check(rc, None, "zk_groth16_verify")
+        return bool(valid.value)
+
+
+class BatchVerifier:
+    """BatchVerifier::verify_batch (core:360-432).  The reference draws one
+    Fr::rand coefficient per proof; pass them as `coeffs` (or an `rng`
+    callable returning Fr ints)."""
+
+    @staticmethod
+    def verify_batch(vk, proofs_and_inputs, coeffs=None, rng=None):
+        k = len(proofs_and_inputs)
+        if coeffs is None:
+            if k and rng is None:
+                raise ValueError("pass coeffs, or an rng")
+            coeffs = [rng() for _ in range(k)]
+        proofs = (_Proof * max(k, 1))()
+        rows = [_fr_rows(inp) for _, inp in proofs_and_inputs]
+        ptrs = (C.c_void_p * max(k, 1))(*[C.c_void_p(r.ctypes.data) for r in rows])
+        lens = (C.c_size_t * max(k, 1))(*[len(r) for r in rows])
+        for i, (pr, _) in enumerate(proofs_and_inputs):
+            proofs[i] = pr._c()
+        co = _fr_rows(coeffs) if k else np.zeros((1, 4), dtype=np.uint64)
+        valid = C.c_int(0)
+        rc = lib().zk_groth16_verify_batch(C.byref(vk.s), proofs, ptrs, lens, C.c_size_t(k), _p(co),
+                                           C.byref(valid))
+        _check(rc, None, "zk_groth16_verify_batch")
+        return bool(valid.value)

@@ -552,7 +552,7 @@ int setup_impl(zk_ctx* ctx, const zk_r1cs_csr* q, const zk_setup_params* P, uint
 static void be48(const uint64_t* l, uint8_t* o) {
   for (int i = 0; i < 48; i++) o[i] = (uint8_t)(l[(47 - i) / 8] >> (8 * ((47 - i) % 8)));
 }
-static bool largest(const uint64_t* c) {
+bool fq_canonical_largest(const uint64_t* c) {
   const uint64_t* m = host::FQ().m;
   uint64_t half[6];
   for (int i = 0; i < 6; i++) half[i] = (m[i] >> 1) | (i < 5 ? (m[i + 1] << 63) : 0);
@@ -572,7 +572,7 @@ void serialize_g1_compressed(const zk_g1_affine& p, uint8_t* out) {
   if (p.infinity) { out[0] = 0xc0; return; }
   be48(p.x, out);
   out[0] |= 0x80;
-  if (largest(p.y)) out[0] |= 0x20;
+  if (fq_canonical_largest(p.y)) out[0] |= 0x20;
 }
 void serialize_g2_compressed(const zk_g2_affine& p, uint8_t* out) {
   std::memset(out, 0, 96);
@@ -580,7 +580,7 @@ void serialize_g2_compressed(const zk_g2_affine& p, uint8_t* out) {
   be48(p.x + 6, out);
   be48(p.x, out + 48);
   out[0] |= 0x80;
-  const bool big = is_zero6(p.y + 6) ? largest(p.y) : largest(p.y + 6);
+  const bool big = is_zero6(p.y + 6) ? fq_canonical_largest(p.y) : fq_canonical_largest(p.y + 6);
   if (big) out[0] |= 0x20;
 }
 

@@ -191,3 +191,15 @@ def test_gpu_proof_verifies_when_untruncated(ctx, zkp):
         assert not zkp.Verifier.verify(crs.vk, proof, [5])
         assert zkp.Proof.deserialize_compressed(proof.serialize_compressed()) == proof
         dpk.free()
+
+
+def test_prove_from_key_file(ctx, zkp, oracle, tmp_path):
+    """A proving key written to and read back from its binary file proves
+    the same bytes (save_proving_key / load_proving_key)."""
+    qap, csr_o, params, r, s, z = _synthetic(zkp, oracle, 8, 4242)
+    crs = zkp.CRS.generate_from_qap(ctx, qap, zkp.SetupParams(*params), 1)
+    zkp.save_proving_key(crs.pk, tmp_path / "pk.bin")
+    back = zkp.load_proving_key(tmp_path / "pk.bin")
+    p1 = zkp.Prover.prove(crs.pk.upload(ctx), zkp.Witness(z, 1), r=r, s=s)
+    p2 = zkp.Prover.prove(back.upload(ctx), zkp.Witness(z, 1), r=r, s=s)
+    assert p1 == p2

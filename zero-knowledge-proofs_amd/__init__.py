@@ -763,3 +763,128 @@ class BatchVerifier:
                                            C.byref(valid))
         _check(rc, None, "zk_groth16_verify_batch")
         return bool(valid.value)
+
+
+# ------------------------------------------------------- file formats ----
+# Binary key files (the reference's CLI writes JSON placeholders instead:
+# crates/groth16-cli/src/lib.rs:157-219).  Little-endian, canonical affine
+# words exactly as they cross the C ABI (13 u64 per G1, 25 per G2), so a
+# 2^24-constraint key (~24 GB) streams through numpy without conversion.
+#   proving key:  b"ZKAMDPK1", u64 x 9 (V, n, num_public, num_constraints,
+#                 a_len, b_len, b2_len, ic_len, h_len), alpha_g1, beta_g1,
+#                 delta_g1, beta_g2, delta_g2, the five base vectors, then the
+#                 QAP (setup:51) as CSR: per matrix u64 nnz, u64 has_val,
+#                 rowptr[nc+1] u64, col[nnz] u32 (+4 pad bytes if nnz odd),
+#                 val[nnz x 4] u64 when has_val
+#   verification key: b"ZKAMDVK1", u64 num_public, ic_len, alpha_g1,
+#                 beta_g2, gamma_g2, delta_g2, ic_g1[ic_len]
+#   proof:        the 192-byte ark compressed encoding (Proof::serialize_compressed)
+_PK_MAGIC, _VK_MAGIC = b"ZKAMDPK1", b"ZKAMDVK1"
+
+
+def _u64s(f, k):
+    a = np.fromfile(f, dtype="<u8", count=k)
+    if len(a) != k:
+        raise ValueError("truncated key file")
+    return a
+
+
+def save_proving_key(pk, path):
+    with open(path, "wb") as f:
+        f.write(_PK_MAGIC)
+        csr = pk.qap.csr
+        np.array([pk.qap.num_variables, pk.qap.domain_size, pk.num_public, csr.num_constraints,
+                  len(pk.a_g1), len(pk.b_g1), len(pk.b_g2), len(pk.ic_g1), len(pk.h_g1)], dtype="<u8").tofile(f)
+        for nm in ("alpha_g1", "beta_g1", "delta_g1", "beta_g2", "delta_g2"):
+            pk.point(nm).astype("<u8").tofile(f)
+        for arr in (pk.a_g1, pk.b_g1, pk.b_g2, pk.ic_g1, pk.h_g1):
+            np.ascontiguousarray(arr, dtype="<u8").tofile(f)
+        for rp, col, val in csr.mats:
+            nnz = len(col)
+            np.array([nnz, val is not None], dtype="<u8").tofile(f)
+            np.ascontiguousarray(rp, dtype="<u8").tofile(f)
+            np.ascontiguousarray(col, dtype="<u4").tofile(f)
+            if nnz & 1:
+                f.write(b"\0" * 4)
+            if val is not None:
+                np.ascontiguousarray(val, dtype="<u8").tofile(f)
+
+
+def load_proving_key(path):
+    with open(path, "rb") as f:
+        if f.read(8) != _PK_MAGIC:
+            raise ValueError(f"{path}: not a proving key file")
+        V, n, npub, nc, la, lb, lb2, lic, lh = (int(x) for x in _u64s(f, 9))
+        pts = [_u64s(f, G1_WORDS) for _ in range(3)] + [_u64s(f, G2_WORDS) for _ in range(2)]
+        arrs = [_u64s(f, k * w).reshape(k, w) for k, w in
+                ((la, G1_WORDS), (lb, G1_WORDS), (lb2, G2_WORDS), (lic, G1_WORDS), (lh, G1_WORDS))]
+        mats = []
+        for _ in range(3):
+            nnz, has_val = (int(x) for x in _u64s(f, 2))
+            rp = _u64s(f, nc + 1).astype(np.uint64)
+            col = np.fromfile(f, dtype="<u4", count=nnz).astype(np.uint32)
+            if len(col) != nnz:
+                raise ValueError("truncated key file")
+            if nnz & 1:
+                f.read(4)
+            val = _u64s(f, 4 * nnz).reshape(nnz, 4).astype(np.uint64) if has_val else None
+            mats.append((rp, col, val))
+    qap = QAP(CSRMatrices(nc, V, mats))
+    if qap.domain_size != n:
+        raise ValueError("key domain does not match its constraint system")
+    pk = ProvingKey(0, 0, npub, qap)
+    pk.a_g1, pk.b_g1, pk.b_g2, pk.ic_g1, pk.h_g1 = (np.ascontiguousarray(a, dtype=np.uint64) for a in arrs)
+    for nm, words in zip(("alpha_g1", "beta_g1", "delta_g1", "beta_g2", "delta_g2"), pts):
+        field = getattr(pk.s, nm)
+        for i, w in enumerate(words):
+            field.w[i] = int(w)
+    return pk
+
+
+def save_verification_key(vk, path):
+    with open(path, "wb") as f:
+        f.write(_VK_MAGIC)
+        np.array([vk.num_public, len(vk.ic_g1)], dtype="<u8").tofile(f)
+        for nm in ("alpha_g1", "beta_g2", "gamma_g2", "delta_g2"):
+            vk.point(nm).astype("<u8").tofile(f)
+        np.ascontiguousarray(vk.ic_g1, dtype="<u8").tofile(f)
+
+
+def load_verification_key(path):
+    with open(path, "rb") as f:
+        if f.read(8) != _VK_MAGIC:
+            raise ValueError(f"{path}: not a verification key file")
+        npub, lic = (int(x) for x in _u64s(f, 2))
+        pts = [_u64s(f, G1_WORDS)] + [_u64s(f, G2_WORDS) for _ in range(3)]
+        ic = _u64s(f, lic * G1_WORDS).reshape(lic, G1_WORDS)
+    vk = VerificationKey.from_points(*pts, ic)
+    vk.num_public = vk.s.num_public = npub
+    return vk
+
+
+# The reference CLI's serde JSON shapes (crates/groth16-cli/src/lib.rs:16-51):
+# coefficients and values are hex strings ("0x" optional).
+def _hex(v):
+    return int(v, 16) % R
+
+
+def r1cs_from_circuit_json(doc):
+    """CircuitDescription {num_variables (without the constant), num_public,
+    constraints: [{a, b, c: [[var, coeff_hex], ...]}]} -> R1CS."""
+    cs = R1CS(int(doc["num_public"]))
+    while cs.num_variables < int(doc["num_variables"]) + 1:
+        cs.allocate_variable()
+    for con in doc["constraints"]:
+        lcs = [LinearCombination({int(v): _hex(c) for v, c in con[m]}) for m in "abc"]
+        cs.enforce_multiplication(*lcs)
+    return cs
+
+
+def witness_from_json(doc):
+    """WitnessData {assignment: [hex], num_public} -> Witness."""
+    return Witness([_hex(x) for x in doc["assignment"]], int(doc["num_public"]))
+
+
+def public_inputs_from_json(doc):
+    """PublicInputs {inputs: [hex]} -> list of ints."""
+    return [_hex(x) for x in doc["inputs"]]

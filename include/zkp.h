@@ -132,6 +132,16 @@ int zk_msm_g2(zk_ctx *ctx, const zk_g2_affine *bases, size_t nbases,
 typedef struct zk_msm_bases zk_msm_bases;
 int zk_msm_g1_upload(zk_ctx *ctx, const zk_g1_affine *bases, size_t n, zk_msm_bases **out);
 int zk_msm_g2_upload(zk_ctx *ctx, const zk_g2_affine *bases, size_t n, zk_msm_bases **out);
+/* Same, plus ceil(scalar_bits / 16) window-shifted copies 2^(16 w) P of every
+ * base (scalar_bits = 0 -> 255): later zk_msm_*_dev calls with scalars of at
+ * most scalar_bits bits sum every digit window into ONE bucket set (one
+ * bucket reduction, no per-window Horner).  Costs ceil(scalar_bits/16) x the
+ * base memory and a one-time precomputation.  No reference counterpart
+ * (fixed-base preprocessing of bases reused across MSMs, as in the prover). */
+int zk_msm_g1_upload_windows(zk_ctx *ctx, const zk_g1_affine *bases, size_t n, uint32_t scalar_bits,
+                             zk_msm_bases **out);
+int zk_msm_g2_upload_windows(zk_ctx *ctx, const zk_g2_affine *bases, size_t n, uint32_t scalar_bits,
+                             zk_msm_bases **out);
 void zk_msm_bases_free(zk_msm_bases *b);
 int zk_msm_g1_dev(zk_ctx *ctx, const zk_msm_bases *bases, const void *d_scalars, size_t n,
                   uint32_t scalar_bits, zk_g1_affine *out);

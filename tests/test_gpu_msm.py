@@ -157,3 +157,53 @@ def test_msm_g2_skewed_scalars(ctx, oracle, pattern):
     sc = np.zeros((n, 4), dtype=np.uint64)
     sc[:, 0] = 1 if pattern == "ones" else np.random.default_rng(3).integers(0, 4, n, dtype=np.uint64)
     assert np.array_equal(ctx.msm_g2(bases, sc, 64), oracle.msm_g2(bases, sc))
+
+
+def _msm_uploaded(zkp, ctx, bases, sc, bits, windows):
+    """zk_msm_g1_upload(_windows) + zk_msm_g1_dev with scalars in HBM."""
+    import ctypes as C
+    import torch
+    L = zkp.lib()
+    hb = C.c_void_p()
+    n = len(bases)
+    if windows is None:
+        zkp._check(L.zk_msm_g1_upload(C.c_void_p(ctx._h), zkp._p(bases), C.c_size_t(n), C.byref(hb)), ctx)
+    else:
+        zkp._check(L.zk_msm_g1_upload_windows(C.c_void_p(ctx._h), zkp._p(bases), C.c_size_t(n),
+                                              C.c_uint32(windows), C.byref(hb)), ctx)
+    d = torch.from_numpy(np.ascontiguousarray(sc, dtype=np.uint64).view(np.int64)).cuda()
+    out = np.zeros(13, dtype=np.uint64)
+    try:
+        zkp._check(L.zk_msm_g1_dev(C.c_void_p(ctx._h), hb, C.c_void_p(d.data_ptr()), C.c_size_t(n),
+                                   C.c_uint32(bits), zkp._p(out)), ctx)
+    finally:
+        L.zk_msm_bases_free(hb)
+    return out
+
+
+@pytest.mark.parametrize("windows", [64, 255, 0])
+@pytest.mark.parametrize("bits", [64, 255])
+@pytest.mark.parametrize("pattern", ["uniform", "ones", "sparse_big"])
+def test_msm_g1_window_upload(ctx, zkp, oracle, lin_bases, windows, bits, pattern):
+    """Bases uploaded with their window-shifted copies (one shared bucket set)
+    give the same point as the plain upload and the closed form; scalars
+    wider than the upload's window bits fall back to per-window buckets."""
+    n = 1 << 14
+    bases = lin_bases[:n].copy()
+    rng = np.random.default_rng(17)
+    if pattern == "uniform":
+        sc = oracle.random_fr(n, 23)
+    else:
+        sc = np.zeros((n, 4), dtype=np.uint64)
+        sc[:, 0] = 1 if pattern == "ones" else rng.integers(0, 2, n, dtype=np.uint64)
+        if pattern == "sparse_big":
+            idx = rng.choice(n, 32, replace=False)
+            sc[idx] = oracle.random_fr(32, 24)
+    if bits == 64:
+        sc[:, 1:] = 0
+    bases[5] = 0
+    bases[5, 12] = 1                       # an infinity base
+    want = _closed_form(oracle, np.where(np.arange(n)[:, None] == 5, 0, sc).astype(np.uint64))
+    got = _msm_uploaded(zkp, ctx, bases, sc, bits, windows)
+    assert np.array_equal(got, want)
+    assert np.array_equal(got, _msm_uploaded(zkp, ctx, bases, sc, bits, None))

@@ -43,7 +43,8 @@ EXPORTS = (
     "zk_groth16_setup_dev_shard", "zk_groth16_prove_partial", "zk_groth16_prove_combine",
     "zk_proof_serialize_compressed", "zk_rccl_unique_id", "zk_ctx_attach_rccl",
     "zk_test_prove_virtual_shards", "zk_proof_deserialize_compressed", "zk_groth16_verify",
-    "zk_groth16_verify_batch", "zk_pairing_product_is_one",
+    "zk_groth16_verify_batch", "zk_pairing_product_is_one", "zk_msm_g1_upload_windows",
+    "zk_msm_g2_upload_windows",
 )
 
 

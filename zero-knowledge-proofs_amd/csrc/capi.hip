@@ -158,20 +158,35 @@ int zk_msm_g2(zk_ctx* ctx, const zk_g2_affine* bases, size_t nb, const zk_fr* sc
   return msm_host<G2>(ctx, bases, nb, sc, ns, bits, out);
 }
 
+// Window-shifted uploads (zk_msm_*_upload_windows): c = 16-bit digit windows,
+// W = ceil(scalar_bits / 16) copies 2^(16 w) P of every base, so every
+// later MSM of <= scalar_bits-bit scalars sums all its windows into ONE
+// bucket set (msm_launch_shared; the prove path's trick, prove.hip).
+constexpr int MSM_UPLOAD_WIN_C = 16;
+
 template <class C, class ABI>
-static int msm_upload(zk_ctx* ctx, const ABI* bases, size_t n, int group, zk_msm_bases** out) {
+static int msm_upload(zk_ctx* ctx, const ABI* bases, size_t n, int group, uint32_t win_bits, zk_msm_bases** out) {
   if (!ctx || !out) return ZK_ERR_ARG;
+  if (win_bits > 256) return ZK_ERR_ARG;
   ZK_GUARD(ctx, {
     std::unique_ptr<zk_msm_bases> b(new zk_msm_bases());
     b->device = ctx->device;
     b->group = group;
     b->n = n;
-    b->bases.ensure(sizeof(typename C::A) * std::max<size_t>(n, 1));
+    const int W = win_bits ? (int)((win_bits + MSM_UPLOAD_WIN_C - 1) / MSM_UPLOAD_WIN_C) : 1;
+    if ((uint64_t)n * W >= 0x7fffffffull) throw Error(ZK_ERR_ARG, "msm: too many window bases");
+    b->bases.ensure(sizeof(typename C::A) * std::max<size_t>(n * W, 1));
     DevBuf raw;
     raw.ensure(sizeof(ABI) * std::max<size_t>(n, 1));
     if (n) {
       ZK_HIP(hipMemcpyAsync(raw.p, bases, sizeof(ABI) * n, hipMemcpyHostToDevice, ctx->stream));
       convert_bases<C>(raw.as<uint64_t>(), b->bases.as<typename C::A>(), n, ctx->stream);
+      if (W > 1) msm_precompute_windows<C>(b->bases.as<typename C::A>(), n, W, MSM_UPLOAD_WIN_C, ctx->stream);
+    }
+    if (W > 1) {
+      b->win = W;
+      b->win_c = MSM_UPLOAD_WIN_C;
+      b->win_bits = win_bits;
     }
     ZK_HIP(hipStreamSynchronize(ctx->stream));
     *out = b.release();
@@ -179,10 +194,18 @@ static int msm_upload(zk_ctx* ctx, const ABI* bases, size_t n, int group, zk_msm
   })
 }
 int zk_msm_g1_upload(zk_ctx* ctx, const zk_g1_affine* bases, size_t n, zk_msm_bases** out) {
-  return msm_upload<G1>(ctx, bases, n, 1, out);
+  return msm_upload<G1>(ctx, bases, n, 1, 0, out);
 }
 int zk_msm_g2_upload(zk_ctx* ctx, const zk_g2_affine* bases, size_t n, zk_msm_bases** out) {
-  return msm_upload<G2>(ctx, bases, n, 2, out);
+  return msm_upload<G2>(ctx, bases, n, 2, 0, out);
+}
+int zk_msm_g1_upload_windows(zk_ctx* ctx, const zk_g1_affine* bases, size_t n, uint32_t scalar_bits,
+                             zk_msm_bases** out) {
+  return msm_upload<G1>(ctx, bases, n, 1, scalar_bits ? scalar_bits : 255, out);
+}
+int zk_msm_g2_upload_windows(zk_ctx* ctx, const zk_g2_affine* bases, size_t n, uint32_t scalar_bits,
+                             zk_msm_bases** out) {
+  return msm_upload<G2>(ctx, bases, n, 2, scalar_bits ? scalar_bits : 255, out);
 }
 void zk_msm_bases_free(zk_msm_bases* b) {
   if (!b) return;
@@ -217,7 +240,11 @@ static int msm_dev(zk_ctx* ctx, const zk_msm_bases* b, const void* d_sc, size_t 
       sw = 1;
     }
     MsmWork& w = ctx->msm[0];
-    msm_launch<C>(w, b->bases.as<typename C::A>(), sc, sw, (uint32_t)n, sw == 1 ? 64 : 255, st);
+    const int mbits = sw == 1 ? 64 : 255;
+    if (b->win > 1 && (uint32_t)mbits <= b->win_bits)   // one bucket set over the shifted copies
+      msm_launch_shared<C>(w, b->bases.as<typename C::A>(), sc, sw, (uint32_t)n, mbits, b->win_c, st);
+    else
+      msm_launch<C>(w, b->bases.as<typename C::A>(), sc, sw, (uint32_t)n, mbits, st);
     msm_download<C>(w, st);
     ZK_HIP(hipStreamSynchronize(st));
     ctx->prof.collect();

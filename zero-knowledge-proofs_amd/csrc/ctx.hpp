@@ -73,5 +73,7 @@ struct zk_msm_bases {
   int device = 0;
   int group = 1;  // 1 = G1, 2 = G2
   size_t n = 0;
-  zk::DevBuf bases;
+  zk::DevBuf bases;   // n points, or win x n window-shifted copies (window-major)
+  int win = 1, win_c = 0;
+  uint32_t win_bits = 0;   // scalars up to this width use the shared bucket set
 };

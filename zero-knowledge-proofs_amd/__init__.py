@@ -23,7 +23,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libzkp_amd.so")
+# ZK_AMD_LIB: an alternative build of the same library (tuning A/B runs)
+LIB_PATH = os.environ.get("ZK_AMD_LIB") or os.path.join(_HERE, "libzkp_amd.so")
 
 R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001  # Fr modulus
 

@@ -179,6 +179,75 @@ ZK_DI XYZZ<F> xyzz_add(const XYZZ<F>& p, const XYZZ<F>& q) {
   return r;
 }
 
+// ---- lane-quad cooperative add (latency-bound reductions) --------------
+// In the bucket-reduction trees a few hundred sums run at once, one or two
+// waves per SIMD, so an add costs its full instruction latency (~14 products
+// issued back to back).  Here the four lanes of a quad hold the same p and q
+// and split each stage's independent products: add-2008-s is 4 stages of
+// <= 4 products (U1 U2 S1 S2 | PP RR ZZ1ZZ2 ZZZ1ZZZ2 | PPP Q ZZ3 | ZZZ3 S1PPP
+// R(Q-X3)), each lane computes one and the results are broadcast inside the
+// quad by DPP moves.  Every lane of a quad must be active and hold the same
+// operands (then every branch below is uniform within the quad).
+template <int K, class F>
+ZK_DI F quad_bcast(const F& v) {
+  constexpr int NW = sizeof(F) / 4;
+  F o;
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(&v);
+  uint32_t* d = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+  for (int k = 0; k < NW; k++)
+    d[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)s[k], K * 0x55, 0xf, 0xf, false);   // quad_perm [K,K,K,K]
+  return o;
+}
+template <class F>
+ZK_DI F quad_sel(const F& a0, const F& a1, const F& a2, const F& a3, uint32_t qi) {
+  constexpr int NW = sizeof(F) / 4;
+  F o;
+  const uint32_t* s0 = reinterpret_cast<const uint32_t*>(&a0);
+  const uint32_t* s1 = reinterpret_cast<const uint32_t*>(&a1);
+  const uint32_t* s2 = reinterpret_cast<const uint32_t*>(&a2);
+  const uint32_t* s3 = reinterpret_cast<const uint32_t*>(&a3);
+  uint32_t* d = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+  for (int k = 0; k < NW; k++) {
+    const uint32_t lo = (qi & 1) ? s1[k] : s0[k];
+    const uint32_t hi = (qi & 1) ? s3[k] : s2[k];
+    d[k] = (qi & 2) ? hi : lo;
+  }
+  return o;
+}
+
+template <class F>
+ZK_DI XYZZ<F> xyzz_add_quad(const XYZZ<F>& p, const XYZZ<F>& q) {
+  if (xyzz_is_inf(p)) return q;
+  if (xyzz_is_inf(q)) return p;
+  const uint32_t qi = threadIdx.x & 3;
+  F m = f_mul(quad_sel(p.X, q.X, p.Y, q.Y, qi), quad_sel(q.ZZ, p.ZZ, q.ZZZ, p.ZZZ, qi));
+  ZK_SB();
+  const F U1 = quad_bcast<0>(m), S1 = quad_bcast<2>(m);
+  const F P = f_sub(quad_bcast<1>(m), U1);
+  const F R = f_sub(quad_bcast<3>(m), S1);
+  if (f_is_zero(P)) {
+    if (f_is_zero(R)) return xyzz_dbl_call(p);
+    XYZZ<F> r; xyzz_set_inf(r); return r;
+  }
+  m = f_mul(quad_sel(P, R, p.ZZ, p.ZZZ, qi), quad_sel(P, R, q.ZZ, q.ZZZ, qi));
+  ZK_SB();
+  const F PP = quad_bcast<0>(m), RR = quad_bcast<1>(m), ZZ12 = quad_bcast<2>(m), ZZZ12 = quad_bcast<3>(m);
+  m = f_mul(quad_sel(P, U1, ZZ12, ZZ12, qi), PP);
+  ZK_SB();
+  XYZZ<F> r;
+  const F PPP = quad_bcast<0>(m), Q = quad_bcast<1>(m);
+  r.ZZ = quad_bcast<2>(m);
+  r.X = f_sub(f_sub(RR, PPP), f_add(Q, Q));
+  const F QX = f_sub(Q, r.X);
+  m = f_mul(quad_sel(ZZZ12, S1, R, R, qi), quad_sel(PPP, PPP, QX, QX, qi));
+  ZK_SB();
+  r.ZZZ = quad_bcast<0>(m);
+  r.Y = f_sub(quad_bcast<2>(m), quad_bcast<1>(m));
+  return r;
+}
+
 template <class F>
 ZK_DI Affine<F> aff_neg(const Affine<F>& a) { return {a.x, f_neg(a.y)}; }
 

@@ -322,13 +322,19 @@ __device__ __forceinline__ uint32_t chunk_len(uint32_t M, uint32_t T) { return M
 //   complete bucket                        -> buckets[g]
 //   run begun by an earlier thread (head)   -> partials[2t]
 //   run continued by a later thread (tail)  -> partials[2t+1]
+// tuning builds: -DZK_ACCUM_WPE=w asks for >= w waves per SIMD (register cap)
+#ifdef ZK_ACCUM_WPE
+#define ZK_ACCUM_ATTR __attribute__((amdgpu_waves_per_eu(ZK_ACCUM_WPE)))
+#else
+#define ZK_ACCUM_ATTR
+#endif
 template <class A>
 struct SegBases {
   const A* p[MSM_MAXSEG];
 };
 
 template <class C>
-__global__ void __launch_bounds__(128) k_msm_accum(SegBases<typename C::A> sb, uint32_t segshift, uint32_t idx_mask,
+__global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum(SegBases<typename C::A> sb, uint32_t segshift, uint32_t idx_mask,
                                                    const uint32_t* __restrict__ ent,
                                                    const uint32_t* __restrict__ key,
                                                    const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
@@ -558,6 +564,146 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_quant(MsmPlan p, con
   if (lane == 0) st_vec(&res[b], v);
 }
 
+// ---- lane-quad reductions (xyzz_add_quad) ------------------------------
+// The same sums with each add split over the 4 lanes of a quad (curve.hpp):
+// one sum per workgroup of RW waves = 16 RW quads.  Quad j folds terms j,
+// j + 16 RW, ... serially, a 4-step __shfl_xor butterfly (lane distances
+// 4..32 keep each lane's quad position) combines a wave, then waves 1..RW-1
+// hand their totals to wave 0 through LDS.  One xyzz_add_quad call site.
+// ZK_RED_QUAD (build-time mask): 1 = quantities, 2 = row/column sums,
+// 4 = G1 fixup use the quad kernels; ZK_RED_QWAVES waves per quad sum.
+#ifndef ZK_RED_QUAD
+#define ZK_RED_QUAD 1
+#endif
+#ifndef ZK_RED_QWAVES
+#define ZK_RED_QWAVES 4
+#endif
+
+template <class X, int RW>
+__device__ __forceinline__ X quad_sum_step(X v, uint32_t it, uint32_t niter, X* xs, bool have, const X& term) {
+  X o;
+  if (it < niter) {
+    if (have) o = term;
+    else xyzz_set_inf(o);
+  } else if (it < niter + 4) {
+    o = shfl_xor_point(v, 4 << (it - niter));
+  } else {
+    const uint32_t k = it - niter - 4, wave = threadIdx.x >> 6;
+    if (k == 0) {
+      if (wave && (threadIdx.x & 63) == 0) xs[wave - 1] = v;
+      __syncthreads();
+    }
+    if (wave == 0) o = xs[k];
+    else xyzz_set_inf(o);
+  }
+  return o;
+}
+
+template <class C, int RW>
+__global__ void __launch_bounds__(64 * RW) k_msm_rowcol_q(MsmPlan p, const uint32_t* __restrict__ off,
+                                                         const typename C::X* __restrict__ buckets,
+                                                         typename C::X* __restrict__ rc) {
+  using X = typename C::X;
+  __shared__ X xs[RW > 1 ? RW - 1 : 1];
+  constexpr uint32_t NQ = 16 * RW;
+  const uint32_t b = blockIdx.x;
+  if (b >= p.nrc) return;   // whole workgroup
+  int w = 0;
+  while (b >= p.rcoff[w + 1]) w++;
+  const uint32_t i = b - p.rcoff[w];
+  const uint32_t rows = 1u << p.kr[w], cols = 1u << p.kc[w];
+  uint32_t len, g0, stride;
+  if (i < rows) {
+    len = cols; g0 = p.boff[w] + i * cols; stride = 1;
+  } else {
+    len = rows; g0 = p.boff[w] + (i - rows); stride = cols;
+  }
+  const uint32_t j = threadIdx.x >> 2;
+  const uint32_t niter = (len + NQ - 1) / NQ;
+  X v;
+  xyzz_set_inf(v);
+#pragma unroll 1
+  for (uint32_t it = 0; it < niter + 4 + (RW - 1); it++) {
+    X term;
+    bool have = false;
+    if (it < niter) {
+      const uint32_t t = it * NQ + j, g = g0 + t * stride;
+      have = t < len && off[g + 1] != off[g];
+      if (have) term = ld_vec(&buckets[g]);
+    }
+    const X o = quad_sum_step<X, RW>(v, it, niter, xs, have, term);
+    v = xyzz_add_quad(v, o);
+  }
+  if (threadIdx.x == 0) st_vec(&rc[b], v);
+}
+
+template <class C, int RW>
+__global__ void __launch_bounds__(64 * RW) k_msm_quant_q(MsmPlan p, const typename C::X* __restrict__ rc,
+                                                        typename C::X* __restrict__ res) {
+  using X = typename C::X;
+  __shared__ X xs[RW > 1 ? RW - 1 : 1];
+  constexpr uint32_t NQ = 16 * RW;
+  const uint32_t b = blockIdx.x;
+  if (b >= p.nq) return;
+  int w = 0;
+  while (b >= p.qoff[w + 1]) w++;
+  const uint32_t q = b - p.qoff[w];
+  const uint32_t kr = p.kr[w], kc = p.kc[w];
+  const uint32_t rows = 1u << kr, cols = 1u << kc;
+  uint32_t len, bit;
+  const X* src;
+  if (q < kr) {               // U^C_q
+    len = rows; src = rc + p.rcoff[w]; bit = q;
+  } else if (q < kr + kc) {   // U^D_{q-kr}
+    len = cols; src = rc + p.rcoff[w] + rows; bit = q - kr;
+  } else {                    // P
+    len = cols; src = rc + p.rcoff[w] + rows; bit = 32;
+  }
+  const uint32_t j = threadIdx.x >> 2;
+  const uint32_t niter = (len + NQ - 1) / NQ;
+  X v;
+  xyzz_set_inf(v);
+#pragma unroll 1
+  for (uint32_t it = 0; it < niter + 4 + (RW - 1); it++) {
+    X term;
+    bool have = false;
+    if (it < niter) {
+      const uint32_t t = it * NQ + j;
+      have = t < len && (bit == 32 || ((t >> bit) & 1));
+      if (have) term = ld_vec(&src[t]);
+    }
+    const X o = quad_sum_step<X, RW>(v, it, niter, xs, have, term);
+    v = xyzz_add_quad(v, o);
+  }
+  if (threadIdx.x == 0) st_vec(&res[b], v);
+}
+
+// k_msm_fixup with one quad per bucket (G1: its waves fit 3 per SIMD, so the
+// 4x lanes cost no extra rounds; G2 keeps the one-thread version).
+template <class C>
+__global__ void __launch_bounds__(128) k_msm_fixup_q(const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
+                                                     uint32_t fix_max, uint32_t* __restrict__ nbig,
+                                                     typename C::X* __restrict__ buckets,
+                                                     const typename C::X* __restrict__ partials) {
+  using X = typename C::X;
+  const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  const bool lead = (threadIdx.x & 3) == 0;
+  if (g >= G) return;   // quad-uniform from here on
+  const uint32_t K = chunk_len(off[G], T);
+  const uint32_t bs = off[g], be = off[g + 1];
+  if (be == bs) return;
+  const uint32_t t0 = bs / K, t1 = (be - 1) / K;
+  if (t0 == t1) return;
+  if (t1 - t0 + 1 > fix_max) {
+    if (lead) atomicAdd(nbig, 1u);
+    return;
+  }
+  X acc = ld_vec(&partials[2 * (size_t)t0 + 1]);
+#pragma unroll 1
+  for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add_quad(acc, ld_vec(&partials[2 * (size_t)t]));
+  if (lead) st_vec(&buckets[g], acc);
+}
+
 // ------------------------------------------------------------ driver -----
 void sort_pairs_u32(void* tmp, size_t& tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
                     const uint32_t* vals_in, uint32_t* vals_out, size_t n, unsigned end_bit, hipStream_t st);
@@ -700,8 +846,13 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
   ph = pf ? pf->begin(st, (w.tag + "msm_merge").c_str(), p.G) : -1;   // buckets split across chunks
   w.nbig.ensure(sizeof(uint32_t));
   ZK_HIP(hipMemsetAsync(w.nbig.p, 0, sizeof(uint32_t), st));
-  k_msm_fixup<C><<<ceil_div(p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), p.G, p.T, p.fix_max,
-                                                      w.nbig.as<uint32_t>(), w.buckets.as<X>(), w.partials.as<X>());
+  if ((ZK_RED_QUAD & 4) && !g2)
+    k_msm_fixup_q<C><<<ceil_div(4 * (size_t)p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), p.G, p.T, p.fix_max,
+                                                                     w.nbig.as<uint32_t>(), w.buckets.as<X>(),
+                                                                     w.partials.as<X>());
+  else
+    k_msm_fixup<C><<<ceil_div(p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), p.G, p.T, p.fix_max,
+                                                        w.nbig.as<uint32_t>(), w.buckets.as<X>(), w.partials.as<X>());
   ZK_LAUNCH_CHECK();
   {
     X* a = w.partials.as<X>();
@@ -720,10 +871,17 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
   }
   if (pf) pf->end(st, ph);
   ph = pf ? pf->begin(st, (w.tag + "msm_bucket_sum").c_str(), p.G) : -1;   // row/col sums + quantities
-  k_msm_rowcol<C><<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.off.as<uint32_t>(),
-                                                                                w.buckets.as<X>(), w.rc.as<X>());
+  constexpr int RW = ZK_RED_QWAVES;
+  if (ZK_RED_QUAD & 2)
+    k_msm_rowcol_q<C, RW><<<p.nrc, 64 * RW, 0, st>>>(p, w.off.as<uint32_t>(), w.buckets.as<X>(), w.rc.as<X>());
+  else
+    k_msm_rowcol<C><<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.off.as<uint32_t>(),
+                                                                                  w.buckets.as<X>(), w.rc.as<X>());
   ZK_LAUNCH_CHECK();
-  k_msm_quant<C><<<ceil_div(p.nq, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.rc.as<X>(), w.res.as<X>());
+  if (ZK_RED_QUAD & 1)
+    k_msm_quant_q<C, RW><<<p.nq, 64 * RW, 0, st>>>(p, w.rc.as<X>(), w.res.as<X>());
+  else
+    k_msm_quant<C><<<ceil_div(p.nq, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.rc.as<X>(), w.res.as<X>());
   ZK_LAUNCH_CHECK();
   if (pf) pf->end(st, ph);
 }

@@ -7,7 +7,13 @@
 namespace zk {
 
 constexpr int NTT_TILE_LOG = 11;  // 2048 elements x 32 B = 64 KiB of LDS per workgroup
-constexpr int NTT_THREADS = 256;
+// Radix of the register rounds (2^NTT_R elements per thread) and threads per
+// tile: one group per thread for a full tile.
+#ifndef ZK_NTT_R
+#define ZK_NTT_R 2
+#endif
+constexpr int NTT_R = ZK_NTT_R;
+constexpr int NTT_THREADS = (1 << NTT_TILE_LOG) >> NTT_R;
 // One radix-2^R round of a tile's sub-transform: local stages
 // [lsb, lsb + R).  Each thread owns whole groups of 2^R elements (rows
 // r0 + m 2^lsb, one column), keeps them in registers for all R stages and
@@ -93,12 +99,12 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(Fr* __restrict__ data,
     st_vec(&sh[k], v);
   }
   __syncthreads();
-  // rounds of 3 stages (2 or 1 for the remainder): DIF top-down, DIT bottom-up
-  const uint32_t full = ns / 3, rem = ns % 3;
+  // rounds of NTT_R stages (fewer for the remainder): DIF top-down, DIT bottom-up
+  const uint32_t full = ns / NTT_R, rem = ns % NTT_R;
   if (DIT) {
     uint32_t lsb = 0;
-    for (uint32_t i = 0; i < full; i++, lsb += 3) {
-      ntt_round<3, true>(sh, tabs.sm, ns, logC, lsb);
+    for (uint32_t i = 0; i < full; i++, lsb += NTT_R) {
+      ntt_round<NTT_R, true>(sh, tabs.sm, ns, logC, lsb);
       __syncthreads();
     }
     if (rem == 2) ntt_round<2, true>(sh, tabs.sm, ns, logC, lsb);
@@ -106,8 +112,8 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(Fr* __restrict__ data,
   } else {
     uint32_t lsb = ns;
     for (uint32_t i = 0; i < full; i++) {
-      lsb -= 3;
-      ntt_round<3, false>(sh, tabs.sm, ns, logC, lsb);
+      lsb -= NTT_R;
+      ntt_round<NTT_R, false>(sh, tabs.sm, ns, logC, lsb);
       __syncthreads();
     }
     if (rem == 2) ntt_round<2, false>(sh, tabs.sm, ns, logC, 0);

@@ -366,6 +366,106 @@ ZK_DI Fq f_inv(const Fq& a) { return fq_inv(a); }
 ZK_DI void f_set_zero(Fq& a) { a = fp_zero<FqParams>(); }
 ZK_DI void f_set_one(Fq& a) { a = fp_one<FqParams>(); }
 
+// ---------------------------------------------------- lane-pair Fq2 ------
+// Fq2h: one Fq2 element spread over the two lanes of an aligned lane pair
+// (lane 2j holds c0, lane 2j+1 holds c1).  Every Fq2 operation is split so
+// both lanes do the same instruction stream on half the data: a product is
+// one coefficient per lane,
+//   lane 0: c0 = REDC(a0 b0 - a1 b1 + 4p^2)   lane 1: c1 = REDC(a1 b0 + a0 b1 + 4p^2)
+// (4p^2 = 0 mod p, so lane 1 may add it too: one code path), with the
+// partner's 28-bit limbs fetched by DPP quad_perm [1,0,3,2].  A G2 XYZZ point
+// is then 48 VGPRs per lane instead of 96, so the G2 bucket accumulation fits
+// two waves per SIMD instead of one.  Both lanes of a pair must be active and
+// take the same branches (every predicate below is combined over the pair).
+struct Fq2h {
+  Fq v;
+};
+ZK_DI uint32_t pair_swap(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+}
+ZK_DI uint32_t pair_half() { return threadIdx.x & 1u; }
+ZK_DI Fq pair_swap(const Fq& a) {
+  Fq o;
+#pragma unroll
+  for (int i = 0; i < 12; i++) o.v[i] = pair_swap(a.v[i]);
+  return o;
+}
+ZK_DI Fq2h f_add(const Fq2h& a, const Fq2h& b) { return {fp_add(a.v, b.v)}; }
+ZK_DI Fq2h f_sub(const Fq2h& a, const Fq2h& b) { return {fp_sub(a.v, b.v)}; }
+ZK_DI Fq2h f_neg(const Fq2h& a) { return {fp_neg(a.v)}; }
+ZK_DI bool f_is_zero(const Fq2h& a) {
+  const uint32_t z = fp_is_zero(a.v) ? 1u : 0u;
+  return (z & pair_swap(z)) != 0;
+}
+ZK_DI void f_set_zero(Fq2h& a) { a.v = fp_zero<FqParams>(); }
+ZK_DI void f_set_one(Fq2h& a) { a.v = pair_half() ? fp_zero<FqParams>() : fp_one<FqParams>(); }
+ZK_DI Fq2h f_mul(const Fq2h& a, const Fq2h& b) {
+  constexpr int M = 14;
+  const bool h = pair_half();
+  uint32_t xa[M], xb[M];
+  unpack28<12, M>(a.v.v, xa);
+  unpack28<12, M>(b.v.v, xb);
+  // lane 0: a0*b0 - a1*b1;  lane 1: a1*b0 + a0*b1  (own a first, partner a second)
+  uint32_t y0[M], y1[M];
+  int32_t nx1[M];
+  const uint32_t neg = h ? 0u : ~0u;
+#pragma unroll
+  for (int i = 0; i < M; i++) {
+    const uint32_t pa = pair_swap(xa[i]), pb = pair_swap(xb[i]);
+    nx1[i] = (int32_t)((pa ^ neg) - neg);
+    y0[i] = h ? pb : xb[i];
+    y1[i] = h ? xb[i] : pb;
+  }
+  uint32_t m[M], r[M];
+  int64_t carry = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * M - 1; k++) {
+    int64_t acc = carry + (int64_t)FqParams::P4SQ28[k];
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < M) {
+        acc += (int64_t)((uint64_t)xa[i] * y0[j]);
+        acc += (int64_t)nx1[i] * (int64_t)(int32_t)y1[j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < M) acc += (int64_t)((uint64_t)m[i] * FqParams::MOD28[j]);
+    }
+    if (k < M) {
+      m[k] = ((uint32_t)acc * FqParams::INV28) & 0x0fffffffu;
+      acc += (int64_t)((uint64_t)m[k] * FqParams::MOD28[0]);
+    } else {
+      r[k - M] = (uint32_t)acc & 0x0fffffffu;
+    }
+    carry = acc >> 28;
+  }
+  r[M - 1] = (uint32_t)(carry + (int64_t)FqParams::P4SQ28[2 * M - 1]);
+  Fq o;
+  pack28<12, M>(r, o.v);
+  return {fp_reduce_once(o)};
+}
+ZK_DI Fq2h f_sqr(const Fq2h& a) {
+  // lane 0: (a0 + a1)(a0 - a1);  lane 1: 2 a1 a0
+  const bool h = pair_half();
+  const Fq p = pair_swap(a.v);
+  const Fq s = fp_add(a.v, p), d = fp_sub(a.v, p);
+  Fq u, w;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    u.v[i] = h ? p.v[i] : s.v[i];
+    w.v[i] = h ? a.v.v[i] : d.v[i];
+  }
+  const Fq t = fq_mul(u, w);
+  const Fq t2 = fp_add(t, t);
+  Fq o;
+#pragma unroll
+  for (int i = 0; i < 12; i++) o.v[i] = h ? t2.v[i] : t.v[i];
+  return {o};
+}
+
 ZK_DI Fq2 f_add(const Fq2& a, const Fq2& b) { return fq2_add(a, b); }
 ZK_DI Fq2 f_sub(const Fq2& a, const Fq2& b) { return fq2_sub(a, b); }
 ZK_DI Fq2 f_mul(const Fq2& a, const Fq2& b) { return fq2_mul(a, b); }

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "msm.hpp"
@@ -378,6 +379,72 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum(SegBases<typena
   else st_vec(&buckets[cur], acc);
 }
 
+// G2 accumulate over lane pairs (Fq2h, ff.hpp): chunk t is owned by lanes
+// 2t, 2t+1, each holding one Fq coefficient of every Fq2 coordinate.  The
+// loop, its branches and the flushes are those of k_msm_accum; the pair's
+// two lanes read and write the two 48-byte halves of each point.
+ZK_DI void st_pair(G2X* p, const XYZZ<Fq2h>& a) {
+  Fq* q = reinterpret_cast<Fq*>(p) + pair_half();
+  st_vec(q + 0, a.X.v);
+  st_vec(q + 2, a.Y.v);
+  st_vec(q + 4, a.ZZ.v);
+  st_vec(q + 6, a.ZZZ.v);
+}
+__global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum_pair(SegBases<G2A> sb, uint32_t segshift,
+                                                                      uint32_t idx_mask,
+                                                                      const uint32_t* __restrict__ ent,
+                                                                      const uint32_t* __restrict__ key,
+                                                                      const uint32_t* __restrict__ off, uint32_t G,
+                                                                      uint32_t T, G2X* __restrict__ buckets,
+                                                                      G2X* __restrict__ partials) {
+  const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
+  const uint32_t h = pair_half();
+  const uint32_t M = off[G];
+  const uint32_t K = chunk_len(M, T);
+  const uint32_t start = t * K;
+  if (t >= T || start >= M) return;   // uniform over the pair
+  const uint32_t end = min(start + K, M);
+  XYZZ<Fq2h> acc;
+  xyzz_set_inf(acc);
+  uint32_t cur = key[start], run_start = start;
+  for (uint32_t e = start; e < end; e++) {
+    const uint32_t g = key[e];
+    const uint32_t en = ent[e];
+    if (g != cur) {
+      const bool head = (run_start == start) && (off[cur] < start);
+      if (head) st_pair(&partials[2 * (size_t)t], acc);
+      else st_pair(&buckets[cur], acc);
+      xyzz_set_inf(acc);
+      cur = g;
+      run_start = e;
+    }
+    if (en == MSM_DUMMY) continue;
+    const uint32_t seg = g >> segshift;
+    const G2A* bases = sb.p[0];
+#pragma unroll
+    for (int k = 1; k < MSM_MAXSEG; k++)
+      if (seg == (uint32_t)k) bases = sb.p[k];
+    const Fq* bp = reinterpret_cast<const Fq*>(&bases[en & idx_mask]) + h;
+    Affine<Fq2h> a{{ld_vec(bp)}, {ld_vec(bp + 2)}};
+    if (en & 0x80000000u) a.y = f_neg(a.y);
+    if (!aff_is_inf(a)) acc = xyzz_madd(acc, a);
+  }
+  const bool head = (run_start == start) && (off[cur] < start);
+  const bool tail = off[cur + 1] > end;
+  if (head) st_pair(&partials[2 * (size_t)t], acc);
+  else if (tail) st_pair(&partials[2 * (size_t)t + 1], acc);
+  else st_pair(&buckets[cur], acc);
+}
+
+// ZK_G2_PAIR=0 keeps the one-lane G2 accumulate (A/B switch)
+static bool g2_pair_mode() {
+  static const bool on = [] {
+    const char* e = getenv("ZK_G2_PAIR");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 // Buckets whose entries span several accumulate chunks.  A bucket over
 // P = t1 - t0 + 1 chunks is tail(t0) + head(t0+1) + ... + head(t1):
 //  * P <= fix_max (the common case: ~1-2): one thread sums the pieces
@@ -704,6 +771,70 @@ __global__ void __launch_bounds__(128) k_msm_fixup_q(const uint32_t* __restrict_
   if (lead) st_vec(&buckets[g], acc);
 }
 
+// ---- lane-pair G2 reductions (Fq2h) -------------------------------------
+// G2 row/column sums and fixup with each add split over a lane pair: half the
+// registers (two waves per SIMD) and half the multiply chain per add on the
+// few hundred latency-bound sums.  Pair j of a wave folds terms j, j + 32,
+// ...; the butterfly's lane distances 2..32 keep each lane's half.
+ZK_DI XYZZ<Fq2h> ld_pair(const G2X* p) {
+  const Fq* q = reinterpret_cast<const Fq*>(p) + pair_half();
+  return {{ld_vec(q + 0)}, {ld_vec(q + 2)}, {ld_vec(q + 4)}, {ld_vec(q + 6)}};
+}
+
+__global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_rowcol_pair(MsmPlan p, const uint32_t* __restrict__ off,
+                                                                       const G2X* __restrict__ buckets,
+                                                                       G2X* __restrict__ rc) {
+  const uint32_t b = blockIdx.x * MSM_RED_WAVES + (threadIdx.x >> 6);
+  const uint32_t pr = (threadIdx.x & 63) >> 1;
+  if (b >= p.nrc) return;   // whole waves
+  int w = 0;
+  while (b >= p.rcoff[w + 1]) w++;
+  const uint32_t i = b - p.rcoff[w];
+  const uint32_t rows = 1u << p.kr[w], cols = 1u << p.kc[w];
+  uint32_t len, g0, stride;
+  if (i < rows) {
+    len = cols; g0 = p.boff[w] + i * cols; stride = 1;
+  } else {
+    len = rows; g0 = p.boff[w] + (i - rows); stride = cols;
+  }
+  const uint32_t niter = (len + 31) >> 5;
+  XYZZ<Fq2h> v;
+  xyzz_set_inf(v);
+#pragma unroll 1
+  for (uint32_t it = 0; it < niter + 5; it++) {
+    XYZZ<Fq2h> o;
+    if (it < niter) {
+      const uint32_t t = it * 32 + pr, g = g0 + t * stride;
+      if (t < len && off[g + 1] != off[g]) o = ld_pair(&buckets[g]);
+      else xyzz_set_inf(o);
+    } else {
+      o = shfl_xor_point(v, 2 << (it - niter));
+    }
+    v = xyzz_add(v, o);
+  }
+  if ((threadIdx.x & 63) < 2) st_pair(&rc[b], v);
+}
+
+__global__ void __launch_bounds__(128) k_msm_fixup_pair(const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
+                                                        uint32_t fix_max, uint32_t* __restrict__ nbig,
+                                                        G2X* __restrict__ buckets, const G2X* __restrict__ partials) {
+  const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
+  if (g >= G) return;   // pair-uniform from here on
+  const uint32_t K = chunk_len(off[G], T);
+  const uint32_t bs = off[g], be = off[g + 1];
+  if (be == bs) return;
+  const uint32_t t0 = bs / K, t1 = (be - 1) / K;
+  if (t0 == t1) return;
+  if (t1 - t0 + 1 > fix_max) {
+    if (!pair_half()) atomicAdd(nbig, 1u);
+    return;
+  }
+  XYZZ<Fq2h> acc = ld_pair(&partials[2 * (size_t)t0 + 1]);
+#pragma unroll 1
+  for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, ld_pair(&partials[2 * (size_t)t]));
+  st_pair(&buckets[g], acc);
+}
+
 // ------------------------------------------------------------ driver -----
 void sort_pairs_u32(void* tmp, size_t& tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
                     const uint32_t* vals_in, uint32_t* vals_out, size_t n, unsigned end_bit, hipStream_t st);
@@ -725,10 +856,14 @@ static uint32_t accum_threads() {
     int dev = 0, cus = 0, per_cu = 0;
     ZK_HIP(hipGetDevice(&dev));
     ZK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_accum<C>, 128, 0));
+    const bool pair = std::is_same<C, G2>::value && g2_pair_mode();   // two lanes per chunk
+    if (pair)
+      ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_accum_pair, 128, 0));
+    else
+      ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_accum<C>, 128, 0));
     double rounds = 1.0;   // tuning: fractions leave room for concurrent streams
     if (const char* e = getenv("ZK_MSM_ROUNDS")) rounds = std::max(0.05, atof(e));
-    return (uint32_t)std::max(1.0, per_cu * cus * 128 * rounds);
+    return (uint32_t)std::max(1.0, per_cu * cus * (pair ? 64 : 128) * rounds);
   }();
   return T;
 }
@@ -837,16 +972,29 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
       const char* e = getenv("ZK_MSM_IDXMASK");
       return e ? (uint32_t)strtoul(e, nullptr, 0) & 0x7fffffffu : 0x7fffffffu;
     }();
-    k_msm_accum<C><<<ceil_div(p.T, 128), 128, 0, st>>>(sb, p.segshift, idx_mask, w.ent.as<uint32_t>(),
-                                                        w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T,
-                                                        w.buckets.as<X>(), w.partials.as<X>());
+    bool pair = false;
+    if constexpr (std::is_same<C, G2>::value) {
+      pair = g2_pair_mode();
+      if (pair)
+        k_msm_accum_pair<<<ceil_div(2 * (size_t)p.T, 128), 128, 0, st>>>(
+            sb, p.segshift, idx_mask, w.ent.as<uint32_t>(), w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T,
+            w.buckets.as<X>(), w.partials.as<X>());
+    }
+    if (!pair)
+      k_msm_accum<C><<<ceil_div(p.T, 128), 128, 0, st>>>(sb, p.segshift, idx_mask, w.ent.as<uint32_t>(),
+                                                          w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T,
+                                                          w.buckets.as<X>(), w.partials.as<X>());
     ZK_LAUNCH_CHECK();
     if (pf) pf->end(st, ph);
   }
   ph = pf ? pf->begin(st, (w.tag + "msm_merge").c_str(), p.G) : -1;   // buckets split across chunks
   w.nbig.ensure(sizeof(uint32_t));
   ZK_HIP(hipMemsetAsync(w.nbig.p, 0, sizeof(uint32_t), st));
-  if ((ZK_RED_QUAD & 4) && !g2)
+  if (g2 && g2_pair_mode())
+    k_msm_fixup_pair<<<ceil_div(2 * (size_t)p.G, 128), 128, 0, st>>>(
+        w.off.as<uint32_t>(), p.G, p.T, p.fix_max, w.nbig.as<uint32_t>(), reinterpret_cast<G2X*>(w.buckets.p),
+        reinterpret_cast<const G2X*>(w.partials.p));
+  else if ((ZK_RED_QUAD & 4) && !g2)
     k_msm_fixup_q<C><<<ceil_div(4 * (size_t)p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), p.G, p.T, p.fix_max,
                                                                      w.nbig.as<uint32_t>(), w.buckets.as<X>(),
                                                                      w.partials.as<X>());
@@ -872,7 +1020,10 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
   if (pf) pf->end(st, ph);
   ph = pf ? pf->begin(st, (w.tag + "msm_bucket_sum").c_str(), p.G) : -1;   // row/col sums + quantities
   constexpr int RW = ZK_RED_QWAVES;
-  if (ZK_RED_QUAD & 2)
+  if (g2 && g2_pair_mode())
+    k_msm_rowcol_pair<<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(
+        p, w.off.as<uint32_t>(), reinterpret_cast<const G2X*>(w.buckets.p), reinterpret_cast<G2X*>(w.rc.p));
+  else if (ZK_RED_QUAD & 2)
     k_msm_rowcol_q<C, RW><<<p.nrc, 64 * RW, 0, st>>>(p, w.off.as<uint32_t>(), w.buckets.as<X>(), w.rc.as<X>());
   else
     k_msm_rowcol<C><<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.off.as<uint32_t>(),

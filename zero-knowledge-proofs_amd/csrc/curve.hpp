@@ -127,7 +127,7 @@ ZK_DI XYZZ<F> xyzz_madd(const XYZZ<F>& p, const Affine<F>& a) {
   XYZZ<F> r;
   r.X = f_sub(f_sub(f_sqr(R), PPP), f_add(Q, Q));
   ZK_SB();
-  r.Y = f_sub(f_mul(R, f_sub(Q, r.X)), f_mul(p.Y, PPP));
+  r.Y = f_mul_sub(R, f_sub(Q, r.X), p.Y, PPP);
   ZK_SB();
   r.ZZ = f_mul(p.ZZ, PP);
   ZK_SB();
@@ -172,9 +172,7 @@ ZK_DI XYZZ<F> xyzz_add(const XYZZ<F>& p, const XYZZ<F>& q) {
   ZK_SB();
   r.X = f_sub(f_sub(f_sqr(R), PPP), f_add(Q, Q));
   ZK_SB();
-  F T = f_mul(S1, PPP);
-  ZK_SB();
-  r.Y = f_sub(f_mul(R, f_sub(Q, r.X)), T);
+  r.Y = f_mul_sub(R, f_sub(Q, r.X), S1, PPP);
   ZK_SB();
   return r;
 }

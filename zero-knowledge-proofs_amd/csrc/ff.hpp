@@ -355,7 +355,19 @@ ZK_DI Fq2 fq2_inv(const Fq2& a) {
   return {fq_mul(a.c0, n), fp_neg(fq_mul(a.c1, n))};
 }
 
+// a*b - c*d with ONE Montgomery reduction (fq_redc2's signed columns and
+// 4p^2 offset): 588 v_mad instead of 784 for two products and a subtraction.
+ZK_DI Fq fq_mul_sub(const Fq& a, const Fq& b, const Fq& c, const Fq& d) {
+  uint32_t xa[14], xb[14], xc[14], xd[14];
+  unpack28<12, 14>(a.v, xa);
+  unpack28<12, 14>(b.v, xb);
+  unpack28<12, 14>(c.v, xc);
+  unpack28<12, 14>(d.v, xd);
+  return fq_redc2<true>(xa, xb, xc, xd);
+}
+
 // Generic field-op shims so curve code is written once for Fq and Fq2.
+ZK_DI Fq f_mul_sub(const Fq& a, const Fq& b, const Fq& c, const Fq& d) { return fq_mul_sub(a, b, c, d); }
 ZK_DI Fq f_add(const Fq& a, const Fq& b) { return fp_add(a, b); }
 ZK_DI Fq f_sub(const Fq& a, const Fq& b) { return fp_sub(a, b); }
 ZK_DI Fq f_mul(const Fq& a, const Fq& b) { return fq_mul(a, b); }
@@ -466,6 +478,10 @@ ZK_DI Fq2h f_sqr(const Fq2h& a) {
   return {o};
 }
 
+ZK_DI Fq2h f_mul_sub(const Fq2h& a, const Fq2h& b, const Fq2h& c, const Fq2h& d) {
+  return f_sub(f_mul(a, b), f_mul(c, d));
+}
+
 ZK_DI Fq2 f_add(const Fq2& a, const Fq2& b) { return fq2_add(a, b); }
 ZK_DI Fq2 f_sub(const Fq2& a, const Fq2& b) { return fq2_sub(a, b); }
 ZK_DI Fq2 f_mul(const Fq2& a, const Fq2& b) { return fq2_mul(a, b); }
@@ -473,5 +489,8 @@ ZK_DI Fq2 f_sqr(const Fq2& a) { return fq2_sqr(a); }
 ZK_DI Fq2 f_neg(const Fq2& a) { return fq2_neg(a); }
 ZK_DI bool f_is_zero(const Fq2& a) { return fq2_is_zero(a); }
 ZK_DI Fq2 f_inv(const Fq2& a) { return fq2_inv(a); }
+ZK_DI Fq2 f_mul_sub(const Fq2& a, const Fq2& b, const Fq2& c, const Fq2& d) {
+  return fq2_sub(fq2_mul(a, b), fq2_mul(c, d));
+}
 ZK_DI void f_set_zero(Fq2& a) { a = fq2_zero(); }
 ZK_DI void f_set_one(Fq2& a) { a = fq2_one(); }

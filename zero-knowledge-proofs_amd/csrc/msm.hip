@@ -863,6 +863,8 @@ static uint32_t accum_threads() {
       ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_accum<C>, 128, 0));
     double rounds = 1.0;   // tuning: fractions leave room for concurrent streams
     if (const char* e = getenv("ZK_MSM_ROUNDS")) rounds = std::max(0.05, atof(e));
+    if (const char* e = getenv(std::is_same<C, G2>::value ? "ZK_MSM_ROUNDS_G2" : "ZK_MSM_ROUNDS_G1"))
+      rounds = std::max(0.05, atof(e));
     return (uint32_t)std::max(1.0, per_cu * cus * (pair ? 64 : 128) * rounds);
   }();
   return T;

@@ -478,8 +478,64 @@ ZK_DI Fq2h f_sqr(const Fq2h& a) {
   return {o};
 }
 
+// a*b - c*d per lane with ONE reduction: four limb products per column,
+//   lane 0: a0 b0 - a1 b1 - c0 d0 + c1 d1,  lane 1: a1 b0 + a0 b1 - c1 d0 - c0 d1,
+// offset by 4p^2 (the sum is > -2p^2 for inputs < p).
 ZK_DI Fq2h f_mul_sub(const Fq2h& a, const Fq2h& b, const Fq2h& c, const Fq2h& d) {
-  return f_sub(f_mul(a, b), f_mul(c, d));
+  constexpr int M = 14;
+  const bool h = pair_half();
+  uint32_t xa[M], xb[M], xc[M], xd[M];
+  unpack28<12, M>(a.v.v, xa);
+  unpack28<12, M>(b.v.v, xb);
+  unpack28<12, M>(c.v.v, xc);
+  unpack28<12, M>(d.v.v, xd);
+  uint32_t y0[M], y1[M], z0[M], z1[M];
+  int32_t na1[M], nc0[M], nc1[M];
+  const uint32_t neg = h ? 0u : ~0u;
+#pragma unroll
+  for (int i = 0; i < M; i++) {
+    const uint32_t pa = pair_swap(xa[i]), pb = pair_swap(xb[i]);
+    const uint32_t pc = pair_swap(xc[i]), pd = pair_swap(xd[i]);
+    na1[i] = (int32_t)((pa ^ neg) - neg);        // lane 0: -a1, lane 1: +a0
+    nc0[i] = -(int32_t)xc[i];                    // -c_own
+    nc1[i] = (int32_t)((pc ^ ~neg) - ~neg);      // lane 0: +c1, lane 1: -c0
+    y0[i] = h ? pb : xb[i];
+    y1[i] = h ? xb[i] : pb;
+    z0[i] = h ? pd : xd[i];
+    z1[i] = h ? xd[i] : pd;
+  }
+  uint32_t m[M], r[M];
+  int64_t carry = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * M - 1; k++) {
+    int64_t acc = carry + (int64_t)FqParams::P4SQ28[k];
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < M) {
+        acc += (int64_t)((uint64_t)xa[i] * y0[j]);
+        acc += (int64_t)na1[i] * (int64_t)(int32_t)y1[j];
+        acc += (int64_t)nc0[i] * (int64_t)(int32_t)z0[j];
+        acc += (int64_t)nc1[i] * (int64_t)(int32_t)z1[j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < M) acc += (int64_t)((uint64_t)m[i] * FqParams::MOD28[j]);
+    }
+    if (k < M) {
+      m[k] = ((uint32_t)acc * FqParams::INV28) & 0x0fffffffu;
+      acc += (int64_t)((uint64_t)m[k] * FqParams::MOD28[0]);
+    } else {
+      r[k - M] = (uint32_t)acc & 0x0fffffffu;
+    }
+    carry = acc >> 28;
+  }
+  r[M - 1] = (uint32_t)(carry + (int64_t)FqParams::P4SQ28[2 * M - 1]);
+  Fq o;
+  pack28<12, M>(r, o.v);
+  return {fp_reduce_once(o)};
 }
 
 ZK_DI Fq2 f_add(const Fq2& a, const Fq2& b) { return fq2_add(a, b); }

@@ -56,7 +56,9 @@ zk_ctx* zk_ctx_create(int device) {
     int lo_prio = 0, hi_prio = 0;
     ZK_HIP(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
     ZK_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio));   // quotient + H
-    ZK_HIP(hipStreamCreateWithPriority(&c->side[0], hipStreamNonBlocking, hi_prio));  // G2 MSM
+    const char* g2p = getenv("ZK_G2_PRIO");   // tuning: "lo" puts the G2 stream at low priority
+    ZK_HIP(hipStreamCreateWithPriority(&c->side[0], hipStreamNonBlocking,
+                                       (g2p && g2p[0] == 'l') ? lo_prio : hi_prio));  // G2 MSM
     for (int i = 1; i < NUM_SIDE; i++) ZK_HIP(hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking, lo_prio));
     ZK_HIP(hipEventCreateWithFlags(&c->ev_quot, hipEventDisableTiming));
     ZK_HIP(hipEventCreateWithFlags(&c->ev_scal, hipEventDisableTiming));

@@ -123,42 +123,45 @@ ZK_DI Fp<P> fp_sub(const Fp<P>& a, const Fp<P>& b) {
 template <class P>
 ZK_DI Fp<P> fp_neg(const Fp<P>& a) { return fp_sub(fp_zero<P>(), a); }
 
-// Montgomery product a*b/R mod m by radix-2^28 product scanning.
-// The 32-bit storage limbs are re-cut into N28 28-bit limbs so that every
-// limb product (< 2^56) accumulates into a 64-bit column sum with a single
-// v_mad_u64_u32 -- no carry flags, no carry chains: a column holds at most
-// 2*N28 products (< 2^61).  Montgomery reduction is interleaved per column
-// (m_k = low 28 bits * -m^-1), so R = 2^(28 N28) (2^392 for Fq, 2^280 for
-// Fr).  Inputs < 2^(32N) with 28-bit limbs < 2^28; output < 2m, reduced once.
-// Measured 2.1x the 32-bit CIOS on gfx950 (tools/mulbench.hip).
-template <int N, int M>
+// Montgomery product a*b/R mod m by radix-2^LB product scanning.
+// The 32-bit storage limbs are re-cut into NL limbs of LB bits (Fq 14 x 28,
+// Fr 9 x 29) so that every limb product (< 2^(2 LB)) accumulates into a
+// 64-bit column sum with a single v_mad_u64_u32 -- no carry flags, no carry
+// chains: a column holds at most 2*NL products (Fq < 2^61, Fr < 2^62.2).
+// Montgomery reduction is interleaved per column (m_k = low LB bits *
+// -m^-1), so R = 2^(LB NL) (2^392 for Fq, 2^261 for Fr).  Inputs < 2^(32N);
+// output < 2m, reduced once.  Measured 2.1x the 32-bit CIOS on gfx950
+// (tools/mulbench.hip); Fr at 9 x 29 bits: 162 instead of 200 v_mad.
+template <int N, int M, int LB = 28>
 ZK_DI void unpack28(const uint32_t (&a)[N], uint32_t (&o)[M]) {
+  constexpr uint32_t MASK = (1u << LB) - 1;
 #pragma unroll
   for (int i = 0; i < M; i++) {
-    const int bit = 28 * i, w = bit >> 5, s = bit & 31;
-    const uint32_t lo = a[w];
+    const int bit = LB * i, w = bit >> 5, s = bit & 31;
+    const uint32_t lo = w < N ? a[w] : 0u;
     const uint32_t hi = (w + 1 < N) ? a[w + 1] : 0u;
     const uint32_t v = s ? __builtin_amdgcn_alignbit(hi, lo, s) : lo;
-    o[i] = v & 0x0fffffffu;
+    o[i] = v & MASK;
   }
 }
-template <int N, int M>
+template <int N, int M, int LB = 28>
 ZK_DI void pack28(const uint32_t (&r)[M], uint32_t (&o)[N]) {
 #pragma unroll
   for (int w = 0; w < N; w++) {
-    const int bit = 32 * w, i = bit / 28, s = bit - 28 * i;   // s in {0,4,...,24}
+    const int bit = 32 * w, i = bit / LB, s = bit - LB * i;   // 0 <= s < LB
     uint32_t v = r[i] >> s;
-    if (i + 1 < M) v |= r[i + 1] << (28 - s);
-    if (s > 24 - 4 && i + 2 < M) v |= r[i + 2] << (56 - s);   // never taken for s <= 24
+    if (i + 1 < M && LB - s < 32) v |= r[i + 1] << (LB - s);
+    if (2 * LB - s < 32 && i + 2 < M) v |= r[i + 2] << (2 * LB - s);
     o[w] = v;
   }
 }
 template <class P>
 ZK_DI Fp<P> fp_mul(const Fp<P>& a, const Fp<P>& b) {
-  constexpr int N = P::N, M = P::N28;
+  constexpr int N = P::N, M = P::NL, LB = P::LB;
+  constexpr uint32_t MASK = (1u << LB) - 1;
   uint32_t x[M], y[M], m[M], r[M];
-  unpack28<N, M>(a.v, x);
-  unpack28<N, M>(b.v, y);
+  unpack28<N, M, LB>(a.v, x);
+  unpack28<N, M, LB>(b.v, y);
   uint64_t carry = 0;
 #pragma unroll
   for (int k = 0; k < 2 * M - 1; k++) {
@@ -171,19 +174,19 @@ ZK_DI Fp<P> fp_mul(const Fp<P>& a, const Fp<P>& b) {
 #pragma unroll
     for (int i = 0; i < M; i++) {
       const int j = k - i;
-      if (i < k && j >= 1 && j < M) acc += (uint64_t)m[i] * P::MOD28[j];
+      if (i < k && j >= 1 && j < M) acc += (uint64_t)m[i] * P::MODL[j];
     }
     if (k < M) {
-      m[k] = ((uint32_t)acc * P::INV28) & 0x0fffffffu;
-      acc += (uint64_t)m[k] * P::MOD28[0];
+      m[k] = ((uint32_t)acc * P::INVL) & MASK;
+      acc += (uint64_t)m[k] * P::MODL[0];
     } else {
-      r[k - M] = (uint32_t)acc & 0x0fffffffu;
+      r[k - M] = (uint32_t)acc & MASK;
     }
-    carry = acc >> 28;
+    carry = acc >> LB;
   }
   r[M - 1] = (uint32_t)carry;
   Fp<P> o;
-  pack28<N, M>(r, o.v);
+  pack28<N, M, LB>(r, o.v);
   return fp_reduce_once(o);
 }
 // Squaring: column k of a^2 is 2 sum_{i<j} a_i a_j (+ a_{k/2}^2), so the
@@ -191,9 +194,10 @@ ZK_DI Fp<P> fp_mul(const Fp<P>& a, const Fp<P>& b) {
 // interleaved Montgomery reduction is unchanged.
 template <class P>
 ZK_DI Fp<P> fp_sqr(const Fp<P>& a) {
-  constexpr int N = P::N, M = P::N28;
+  constexpr int N = P::N, M = P::NL, LB = P::LB;
+  constexpr uint32_t MASK = (1u << LB) - 1;
   uint32_t x[M], m[M], r[M];
-  unpack28<N, M>(a.v, x);
+  unpack28<N, M, LB>(a.v, x);
   uint64_t carry = 0;
 #pragma unroll
   for (int k = 0; k < 2 * M - 1; k++) {
@@ -208,19 +212,19 @@ ZK_DI Fp<P> fp_sqr(const Fp<P>& a) {
 #pragma unroll
     for (int i = 0; i < M; i++) {
       const int j = k - i;
-      if (i < k && j >= 1 && j < M) acc += (uint64_t)m[i] * P::MOD28[j];
+      if (i < k && j >= 1 && j < M) acc += (uint64_t)m[i] * P::MODL[j];
     }
     if (k < M) {
-      m[k] = ((uint32_t)acc * P::INV28) & 0x0fffffffu;
-      acc += (uint64_t)m[k] * P::MOD28[0];
+      m[k] = ((uint32_t)acc * P::INVL) & MASK;
+      acc += (uint64_t)m[k] * P::MODL[0];
     } else {
-      r[k - M] = (uint32_t)acc & 0x0fffffffu;
+      r[k - M] = (uint32_t)acc & MASK;
     }
-    carry = acc >> 28;
+    carry = acc >> LB;
   }
   r[M - 1] = (uint32_t)carry;
   Fp<P> o;
-  pack28<N, M>(r, o.v);
+  pack28<N, M, LB>(r, o.v);
   return fp_reduce_once(o);
 }
 

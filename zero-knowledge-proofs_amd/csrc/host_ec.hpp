@@ -101,7 +101,7 @@ inline Fr fr_inv(const Fr& a) {
   return fr_pow(a, e, 256);
 }
 inline Fr fr_from_u64(uint64_t v) { uint64_t c[4] = {v, 0, 0, 0}; return fr_to_mont(c); }
-// host Montgomery (R = 2^256) -> device Montgomery (R = 2^280)
+// host Montgomery (R = 2^256) -> device Montgomery (R = 2^261)
 inline Fr fr_to_dev(const Fr& h) {
   Fr k;
   for (int i = 0; i < 4; i++) k.l[i] = (uint64_t)FrHostParams::TO_DEV[2 * i] | ((uint64_t)FrHostParams::TO_DEV[2 * i + 1] << 32);

@@ -488,6 +488,9 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       waits.push_back(grp[0]);
     };
     auto has_h = [](const std::vector<int>& grp) { return std::find(grp.begin(), grp.end(), (int)MSM_H) != grp.end(); };
+    // ZK_PROVE_SCHED=4: the quotient's kernels are queued first (host launch
+    // order only, no waits), then the G2 MSM and the groups
+    if (sched == 4) run_quotient();
     if (sched == 3) {
       launch_slot(MSM_B2, st);
     } else if (sched != 1) {
@@ -508,7 +511,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       }
       launch_group(grp, gs);
     }
-    run_quotient();
+    if (sched != 4) run_quotient();
     if (sched == 1) {
       ZK_HIP(hipEventRecord(ctx->ev_quot, st));
       ZK_HIP(hipStreamWaitEvent(s2, ctx->ev_quot, 0));

@@ -82,11 +82,13 @@ def phase_table(prof):
 
 
 # VALU view of the same kernel: every mixed add (madd-2008-s) in the prove's
-# G1 MSMs is 10 Fq multiplications of 14 x 14 radix-2^28 limb products plus
-# 14 x 14 for the Montgomery reduction = 3920 v_mad_u64_u32; a prove MSM has
-# 4 digit windows (64-bit scalars, c = 16).  Peak: tools/mulbench.hip, best
-# radix-2^28 variant, 72.2 G Fq-mul/s x 392 = 28.3 T v_mad_u64_u32/s.
-MADS_PER_MADD = 3920
+# G1 MSMs is 8 Fq products of 14 x 14 radix-2^28 limb products (196 v_mad
+# each; Y3 = R(Q-X3) - Y1 PPP counts two), 2 squarings (105 each) and 9
+# Montgomery reductions of 196 (Y3's two products share one) = 3542
+# v_mad_u64_u32; a prove MSM has 4 digit windows (64-bit scalars, c = 16).
+# Peak: tools/mulbench.hip, best radix-2^28 variant, 72.2 G Fq-mul/s x 392 =
+# 28.3 T v_mad_u64_u32/s.
+MADS_PER_MADD = 8 * 196 + 2 * 105 + 9 * 196
 PROVE_WINDOWS = 4
 VALU_PEAK_TMADS = 28.3
 

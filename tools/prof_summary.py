@@ -79,7 +79,7 @@ def pmc(fetch_db, write_db, out):
            "kernels": kernels}
     for k in kernels:
         if k.startswith("k_msm_accum"):
-            tag = "g2" if "G2" in k else "g1"
+            tag = "g2" if ("G2" in k or "pair" in k) else "g1"   # k_msm_accum_pair: G2
             res[f"msm_accum_{tag}_bytes_per_launch"] = kernels[k]["traffic_bytes_per_launch"]
     json.dump(res, open(out, "w"), indent=1)
     for k, v in kernels.items():

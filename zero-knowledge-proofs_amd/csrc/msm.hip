@@ -436,6 +436,16 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum_pair(SegBases<G
   else st_pair(&buckets[cur], acc);
 }
 
+// G1 row/column sums over lane quads when there are at most this many sums
+// (ZK_RC_QUAD_MAX): few sums leave most SIMDs idle, so the 4x lanes are free
+static uint32_t rowcol_quad_max() {
+  static const uint32_t v = [] {
+    const char* e = getenv("ZK_RC_QUAD_MAX");
+    return e ? (uint32_t)strtoul(e, nullptr, 0) : 600u;   // single-window G1 MSMs (H: 512 sums)
+  }();
+  return v;
+}
+
 // ZK_G2_PAIR=0 keeps the one-lane G2 accumulate (A/B switch)
 static bool g2_pair_mode() {
   static const bool on = [] {
@@ -1025,7 +1035,7 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
   if (g2 && g2_pair_mode())
     k_msm_rowcol_pair<<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(
         p, w.off.as<uint32_t>(), reinterpret_cast<const G2X*>(w.buckets.p), reinterpret_cast<G2X*>(w.rc.p));
-  else if (ZK_RED_QUAD & 2)
+  else if ((ZK_RED_QUAD & 2) || (!g2 && p.nrc <= rowcol_quad_max()))
     k_msm_rowcol_q<C, RW><<<p.nrc, 64 * RW, 0, st>>>(p, w.off.as<uint32_t>(), w.buckets.as<X>(), w.rc.as<X>());
   else
     k_msm_rowcol<C><<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.off.as<uint32_t>(),

@@ -183,6 +183,75 @@ void ntt_dit(Fr* d, const NttDomain& dom, bool inv, hipStream_t st, Prof* pf) {
   if (pf) pf->end(st, ph);
 }
 
+// iNTT -> coset shift -> NTT (the quotient's per-polynomial round trip):
+// the last DIF pass and the first DIT pass both work on the same contiguous
+// 2^ns-element tiles, so ONE kernel runs the DIF stages with the inverse
+// twiddles, multiplies each element p by tab[bitrev(p)] (n^-1 g^i) and runs
+// the DIT stages with the forward twiddles while the tile stays in LDS: two
+// HBM round trips and the separate scale pass disappear.
+__global__ void __launch_bounds__(NTT_THREADS) k_ntt_tile_shift(Fr* __restrict__ data, const Fr* __restrict__ ism,
+                                                               const Fr* __restrict__ sm,
+                                                               const Fr* __restrict__ tab, uint32_t log_n,
+                                                               uint32_t ns) {
+  extern __shared__ uint4 sh_raw[];
+  Fr* sh = reinterpret_cast<Fr*>(sh_raw);
+  const uint32_t tile_elems = 1u << ns;
+  const size_t base = (size_t)blockIdx.x << ns;
+  for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) st_vec(&sh[k], ld_vec(&data[base + k]));
+  __syncthreads();
+  const uint32_t full = ns / NTT_R, rem = ns % NTT_R;
+  uint32_t lsb = ns;
+  for (uint32_t i = 0; i < full; i++) {
+    lsb -= NTT_R;
+    ntt_round<NTT_R, false>(sh, ism, ns, 0, lsb);
+    __syncthreads();
+  }
+  if (rem == 2) ntt_round<2, false>(sh, ism, ns, 0, 0);
+  if (rem == 1) ntt_round<1, false>(sh, ism, ns, 0, 0);
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) {
+    const uint32_t p = (uint32_t)(base + k);
+    st_vec(&sh[k], fp_mul(ld_vec(&sh[k]), ld_vec(&tab[bitrev32(p, log_n)])));
+  }
+  __syncthreads();
+  lsb = 0;
+  for (uint32_t i = 0; i < full; i++, lsb += NTT_R) {
+    ntt_round<NTT_R, true>(sh, sm, ns, 0, lsb);
+    __syncthreads();
+  }
+  if (rem == 2) ntt_round<2, true>(sh, sm, ns, 0, lsb);
+  if (rem == 1) ntt_round<1, true>(sh, sm, ns, 0, lsb);
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) st_vec(&data[base + k], ld_vec(&sh[k]));
+}
+
+void ntt_coset_shift(Fr* d, const NttDomain& dom, const Fr* tab, hipStream_t st, Prof* pf) {
+  const uint32_t L = dom.log_n;
+  if (L == 0) {
+    fr_scale_table(d, tab, 0, true, st);
+    return;
+  }
+  const int ph = pf ? pf->begin(st, "ntt", (uint64_t)2 << L) : -1;
+  const NttTabs ti = tabs_of(dom, true), tf = tabs_of(dom, false);
+  const std::vector<uint32_t> plan = pass_plan(L);
+  // inverse transform: every DIF pass but the last (contiguous) one
+  uint32_t s_hi = L;
+  for (size_t i = 0; i + 1 < plan.size(); i++) {
+    run_pass(false, d, ti, L, s_hi - plan[i], plan[i], st);
+    s_hi -= plan[i];
+  }
+  const uint32_t ns = plan.back();   // s_hi == ns here: the contiguous pass
+  k_ntt_tile_shift<<<(uint32_t)((1ull << L) >> ns), NTT_THREADS, sizeof(Fr) << ns, st>>>(d, ti.sm, tf.sm, tab, L, ns);
+  ZK_LAUNCH_CHECK();
+  // forward transform: every DIT pass but the first (contiguous) one
+  uint32_t s_lo = ns;
+  for (size_t i = plan.size() - 1; i-- > 0;) {
+    run_pass(true, d, tf, L, s_lo, plan[i], st);
+    s_lo += plan[i];
+  }
+  if (pf) pf->end(st, ph);
+}
+
 // ------------------------------------------------------------ tables -----
 __device__ __forceinline__ Fr fr_pow_u64(Fr b, uint64_t e) {
   Fr acc = fp_one<FrParams>();

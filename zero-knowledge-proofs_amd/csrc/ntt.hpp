@@ -65,6 +65,10 @@ inline NttTabs tabs_of(const NttDomain& dom, bool inv) {
 void ntt_dif(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st, Prof* pf = nullptr);
 void ntt_dit(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st, Prof* pf = nullptr);
 
+// d <- NTT(tab[bitrev(i)] * iNTT(d)) with the inverse DIF's last pass, the
+// scale and the forward DIT's first pass fused into one tile kernel (the
+// quotient's coefficients -> coset evaluations step; tab = n^-1 g^i).
+void ntt_coset_shift(Fr* d_data, const NttDomain& dom, const Fr* d_tab, hipStream_t st, Prof* pf = nullptr);
 // Elementwise helpers
 void fr_to_mont(const uint64_t* d_canon, Fr* d_out, size_t n, hipStream_t st);
 void fr_from_mont(const Fr* d_in, uint64_t* d_canon, size_t n, hipStream_t st);

@@ -323,12 +323,23 @@ static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipS
   ZK_LAUNCH_CHECK();
   pf->end(st, ph);
   Fr* v[3] = {ctx->qa.as<Fr>(), ctx->qb.as<Fr>(), ctx->qc.as<Fr>()};
+  // per polynomial: iNTT (coefficients * n, bit-reversed), * n^-1 g^i, NTT
+  // (evaluations on the coset g<w>, natural order) -- ZK_NTT_FUSE=0 runs the
+  // three steps as separate passes
+  static const bool fuse = [] {
+    const char* e = getenv("ZK_NTT_FUSE");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
   for (int k = 0; k < 3; k++) {
-    ntt_dif(v[k], dom, /*inverse twiddles*/ true, st, pf);               // coefficients * n, bit-reversed
+    if (fuse) {
+      ntt_coset_shift(v[k], dom, dom.gpow.as<Fr>(), st, pf);
+      continue;
+    }
+    ntt_dif(v[k], dom, /*inverse twiddles*/ true, st, pf);
     ph = pf->begin(st, "quotient_misc", n);
-    fr_scale_table(v[k], dom.gpow.as<Fr>(), pk->log_n, true, st);        // * n^-1 g^i
+    fr_scale_table(v[k], dom.gpow.as<Fr>(), pk->log_n, true, st);
     pf->end(st, ph);
-    ntt_dit(v[k], dom, false, st, pf);                                   // evaluations on g<w>, natural
+    ntt_dit(v[k], dom, false, st, pf);
   }
   ph = pf->begin(st, "quotient_misc", n);
   k_quot_pointwise<<<ceil_div(n, 256), 256, 0, st>>>(v[0], v[1], v[2], dom.zinv.as<Fr>(), n);

@@ -1,25 +1,34 @@
-"""Benchmark: Groth16 prove constraints/s on the synthetic 2^20-constraint
-R1CS (BASELINE.json configs[3]; circuit of crates/groth16-cli/src/lib.rs:57-70),
-plus G1 MSM scalar-point pairs/s at 2^20 (configs[1]) on rank 0.
+"""Benchmark: Groth16 prove constraints/s on the synthetic R1CS of
+crates/groth16-cli/src/lib.rs:57-70 (BASELINE.json configs[3] at one GPU,
+configs[4] on N > 1), plus G1 MSM scalar-point pairs/s at 2^20 (configs[1])
+and the 2^22 Fr NTT (configs[2]) on rank 0 of a one-GPU run.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--log-n 20]
+  python bench.py [--gpus 1] [--steps K] [--warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...
 
 A step = one full prove (quotient NTTs + 5 MSMs + host tail) with the proving
-key and witness already resident in HBM.  N > 1: weak scaling -- the circuit
-has N * 2^log_n constraints, every rank holds 1/N of every base vector
-(GPU setup of its shard), computes its 1/N of the quotient
-(four-step transforms with three RCCL all-to-alls inside the library, H
-coefficients i = rank mod N), runs its MSM shard, and the 1.5 KB partial
-accumulators meet in ONE all-gather over RCCL (the torch.distributed "nccl"
-backend) before the fold.  Rank 0 prints one JSON
-line.  The CPU baseline leg times the C restatement (oracle/, single thread)
-on a bounded sample of the same workload.
+key and the witness already resident in HBM.
+
+  N = 1  the 2^20-constraint prove (configs[3]); its own timed proof is
+         checked bit for bit against the C oracle (oracle/, all host cores)
+         proving from the same key, witness, r and s.
+  N > 1  strong scaling (default): ONE 2^24-constraint circuit (configs[4],
+         --total-log-n) sharded over the N ranks -- every rank holds 1/N of
+         every base vector (GPU setup of its shard), computes its 1/N of the
+         quotient (four-step transforms with three RCCL all-to-alls inside the
+         library; H coefficients i = rank mod N) and its MSM shard; the 1.5 KB
+         partial accumulators meet in ONE all-gather over RCCL before the
+         fold.  --scaling weak keeps 2^log_n constraints per GPU instead.
+
+Rank 0 prints one JSON line.  The CPU baseline leg times the C restatement
+(oracle/, test infrastructure) single-threaded on a bounded sample and on all
+host cores at the full 2^20 size.
 """
 import argparse
 import importlib
 import json
 import os
+import platform
 import sys
 import time
 
@@ -44,8 +53,7 @@ def random_fr(rng, n):
     """n uniform canonical Fr (rejection on the top limb), (n, 4) uint64."""
     out = np.empty((n, 4), dtype=np.uint64)
     filled = 0
-    rbytes = R.to_bytes(32, "little")
-    top = int.from_bytes(rbytes[24:], "little")
+    top = R >> 192
     while filled < n:
         m = int((n - filled) * 1.1) + 16
         w = rng.integers(0, 2 ** 64, size=(m, 4), dtype=np.uint64)
@@ -57,24 +65,18 @@ def random_fr(rng, n):
     return out
 
 
-def synthetic_witness(n, seed):
-    """z = [1, x_0, y_0, x_0 y_0, ...] with uniform x, y (numpy + Python ints for x*y)."""
-    rng = np.random.default_rng(seed)
-    xy = random_fr(rng, 2 * n)
-    ints = [int.from_bytes(row.tobytes(), "little") for row in xy]
-    z = np.zeros((3 * n + 1, 4), dtype=np.uint64)
-    z[0, 0] = 1
-    z[1::3] = xy[0::2]
-    z[2::3] = xy[1::2]
-    prod = [(ints[2 * j] * ints[2 * j + 1]) % R for j in range(n)]
-    z[3::3] = np.frombuffer(b"".join(p.to_bytes(32, "little") for p in prod), dtype=np.uint64).reshape(-1, 4)
-    return z
-
-
 def setup_params(seed):
     rng = np.random.default_rng(seed)
     vals = [int.from_bytes(r.tobytes(), "little") for r in random_fr(rng, 7)]
     return vals[:5], vals[5], vals[6]
+
+
+def prove_msm_pairs(n):
+    """Scalar-point pairs of the reference's five MSMs for the synthetic
+    circuit (V = 3n+1, num_public = 1; core:164-265): G1 = pi_A (V+2) + B_1
+    (V+1) + H (n-1: coefficient n-1 is 0) + pi_C (V-2 ic terms + 3) = 10n+6,
+    G2 = pi_B (V+2) = 3n+3."""
+    return 10 * n + 6, 3 * n + 3
 
 
 def phase_table(prof):
@@ -93,71 +95,131 @@ PROVE_WINDOWS = 4
 VALU_PEAK_TMADS = 28.3
 
 
-def roofline_from(prof):
-    """Dominant kernel: k_msm_accum<G1> (bucket accumulation of the four G1
-    MSMs), priced at SURVEY 8(d)'s 128 B per scalar-point pair."""
+def traffic_for(log_n):
+    """HBM bytes per k_msm_accum<G1> launch from the FETCH/WRITE passes at
+    THIS size (profiles/pmc_traffic_2p<log_n>.json), else None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_traffic_2p{log_n}.json")
+    if not os.path.exists(path):
+        return None, None
+    try:
+        d = json.load(open(path))
+        return d.get("msm_accum_g1_bytes_per_launch"), os.path.relpath(path, ROOT)
+    except Exception:
+        return None, None
+
+
+def roofline_from(prof, log_n, overlapped=None):
+    """Dominant kernel: k_msm_accum<G1> (bucket accumulation of the G1 MSMs:
+    the A+B1+IC batch and H), priced at SURVEY 8(d)'s 128 B per scalar-point
+    pair.  `prof` comes from proves run with every kernel in order on one
+    stream (zk_ctx_set_schedule 3), so a launch's HIP-event span is the
+    kernel's own duration; `overlapped` (the timed region's four-stream
+    schedule) is reported beside it."""
     g1 = prof.get("msm_accum_g1", {"ms": 0.0, "launches": 0, "units": 0})
     ms, launches, units = g1["ms"], g1["launches"], g1["units"]
     if ms <= 0 or launches == 0:
         return None
     algo_bytes = G1_PAIR_BYTES * units
     achieved = algo_bytes / (ms / 1e3) / 1e9
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tpath):
-        try:
-            traffic = json.load(open(tpath)).get("msm_accum_g1_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic, tsrc = traffic_for(log_n)
     tmads = units * PROVE_WINDOWS * MADS_PER_MADD / (ms / 1e3) / 1e12
-    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-            "kernel": "k_msm_accum<G1>",
-            "algorithmic_bytes_per_launch": int(algo_bytes / launches),
-            "avg_launch_ms": round(ms / launches, 4),
-            "valu": {"achieved_tmad_per_s": round(tmads, 2), "peak_tmad_per_s": VALU_PEAK_TMADS,
-                     "frac": round(tmads / VALU_PEAK_TMADS, 4)},
-            "note": "integer-VALU bound (381-bit Montgomery products), not HBM; see DESIGN.md"}
+    out = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+           "traffic_source": tsrc, "kernel": "k_msm_accum<G1>",
+           "algorithmic_bytes_per_launch": int(algo_bytes / launches),
+           "avg_launch_ms": round(ms / launches, 4), "launches": launches,
+           "schedule": "serial (zk_ctx_set_schedule 3): one stream, kernels in order",
+           "valu": {"achieved_tmad_per_s": round(tmads, 2), "peak_tmad_per_s": VALU_PEAK_TMADS,
+                    "frac": round(tmads / VALU_PEAK_TMADS, 4)},
+           "note": "integer-VALU bound (381-bit Montgomery products), not HBM; see DESIGN.md"}
+    if overlapped:
+        o = overlapped.get("msm_accum_g1")
+        if o and o["launches"]:
+            out["overlapped_avg_launch_ms"] = round(o["ms"] / o["launches"], 4)
+    return out
 
 
-def cpu_baseline(zkp, ctx, log_n, seed):
-    """Oracle (C restatement, single thread) prove on a 2^log_n sample of the same workload."""
+def host_cpu():
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model
+
+
+def oracle_pk(oracle, pk):
+    V, n = pk.qap.num_variables, pk.qap.domain_size
+    opk = oracle.PK(V, n, pk.num_public)
+    for nm in ("a_g1", "b_g1", "b_g2", "h_g1"):
+        getattr(opk, nm)[:] = getattr(pk, nm)
+    opk.ic_g1[:len(pk.ic_g1)] = pk.ic_g1
+    for nm in ("alpha_g1", "beta_g1", "delta_g1", "beta_g2", "delta_g2"):
+        arr = getattr(opk.s, nm)
+        for i, x in enumerate(pk.point(nm)):
+            arr[i] = int(x)
+    opk.s.a_len, opk.s.b_len, opk.s.b2_len = len(pk.a_g1), len(pk.b_g1), len(pk.b_g2)
+    opk.s.ic_len, opk.s.h_len, opk.s.num_public = len(pk.ic_g1), len(pk.h_g1), pk.num_public
+    return opk
+
+
+def cpu_baseline(zkp, ctx, n, params, r, s, z_host, gpu_proof, log_n_1t, seed):
+    """The oracle (C restatement of the reference prover, test infrastructure)
+    timed on this box's host cores:
+      all cores  the full 2^20 prove on the bench's own key / witness / r / s,
+                 which also checks the bench's timed proof bit for bit;
+      1 thread   the reference's arkworks build has no `parallel` feature
+                 (Cargo.lock:101-113,161-170): a bounded 2^log_n_1t sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import binding as oracle   # cpu_baseline leg only
-    n = 1 << log_n
-    params, r, s = setup_params(seed)
     qap = zkp.QAP(zkp.CSRMatrices.synthetic(n))
-    crs = zkp.CRS.generate_from_qap(ctx, qap, zkp.SetupParams(*params), 1)   # pk built on GPU (not timed)
-    opk = oracle.PK(qap.num_variables, n, 1)
-    for nm in ("a_g1", "b_g1", "b_g2", "h_g1"):
-        getattr(opk, nm)[:] = getattr(crs.pk, nm)
-    opk.ic_g1[:len(crs.pk.ic_g1)] = crs.pk.ic_g1
-    for nm in ("alpha_g1", "beta_g1", "delta_g1", "beta_g2", "delta_g2"):
-        w = crs.pk.point(nm)
-        arr = getattr(opk.s, nm)
-        for i, x in enumerate(w):
-            arr[i] = int(x)
-    opk.s.a_len = opk.s.b_len = opk.s.b2_len = qap.num_variables
-    opk.s.ic_len, opk.s.h_len, opk.s.num_public = len(crs.pk.ic_g1), n, 1
+    crs = zkp.CRS.generate_from_qap(ctx, qap, zkp.SetupParams(*params), 1)   # same key, host copy (not timed)
+    opk = oracle_pk(oracle, crs.pk)
+    del crs
     csr = oracle.CSR.synthetic(n)
-    z = synthetic_witness(n, seed + 1)
+    nt = oracle.default_threads()
+    oracle.set_threads(nt)
     t0 = time.perf_counter()
-    rc, proof = oracle.prove(opk, csr, z, 1, r, s)
-    dt = time.perf_counter() - t0
+    rc, proof = oracle.prove(opk, csr, z_host, 1, r, s)
+    dt_all = time.perf_counter() - t0
+    del opk
     if rc != 0:
         raise RuntimeError(f"oracle prove failed: {rc}")
-    # same pk / z / r / s on the GPU must give the same bytes
-    dpk = crs.pk.upload(ctx)
-    gproof = zkp.Prover.prove(dpk, zkp.Witness(z, 1), r=r, s=s)
-    dpk.free()
-    return {"value": round(n / dt, 2), "unit": "constraints/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/zk_oracle.c prove() of the 2^{log_n}-constraint synthetic circuit, "
-                      f"single thread (reference arkworks build has no `parallel`), {dt:.2f} s",
-            "bit_exact_vs_gpu": bool(np.array_equal(gproof.words, proof))}
+    exact = bool(np.array_equal(gpu_proof.words, proof))
+    # single thread, bounded sample of the same workload
+    n1 = 1 << log_n_1t
+    qap1 = zkp.QAP(zkp.CSRMatrices.synthetic(n1))
+    crs1 = zkp.CRS.generate_from_qap(ctx, qap1, zkp.SetupParams(*params), 1)
+    opk1 = oracle_pk(oracle, crs1.pk)
+    z1 = ctx.synthetic_witness(n1, seed).cpu().numpy().view(np.uint64)
+    oracle.set_threads(1)
+    t0 = time.perf_counter()
+    rc, proof1 = oracle.prove(opk1, oracle.CSR.synthetic(n1), z1, 1, r, s)
+    dt_1 = time.perf_counter() - t0
+    oracle.set_threads(nt)
+    dpk1 = crs1.pk.upload(ctx)
+    g1 = zkp.Prover.prove(dpk1, zkp.Witness(z1, 1), r=r, s=s)
+    dpk1.free()
+    cpu = host_cpu()
+    return {"value": round(n / dt_all, 2), "unit": "constraints/s", "cores": nt, "kind": "port",
+            "sample": f"oracle/zk_oracle.c prove() of the full 2^{n.bit_length() - 1}-constraint circuit on "
+                      f"{nt} threads (OpenMP: MSM point chunks, FFT butterflies), {dt_all:.2f} s, same pk/z/r/s "
+                      f"as the GPU's timed proof",
+            "cpu_model": cpu, "host_cpus_visible": os.cpu_count(),
+            "bit_exact_vs_gpu": exact,
+            "single_thread": {"value": round(n1 / dt_1, 2), "unit": "constraints/s", "cores": 1,
+                              "sample": f"2^{log_n_1t}-constraint prove, 1 thread (the reference's build), "
+                                        f"{dt_1:.2f} s",
+                              "bit_exact_vs_gpu": bool(np.array_equal(g1.words, proof1))}}
 
 
 def msm_g1_bench(zkp, ctx, log_n, steps, warmup, seed):
     """configs[1]: G1 MSM, 2^log_n bases, uniform full-width scalars, inputs in HBM."""
+    import ctypes as C
     import torch
     n = 1 << log_n
     # 2^log_n distinct bases: h_g1 of a GPU setup on an n-constraint circuit
@@ -168,7 +230,6 @@ def msm_g1_bench(zkp, ctx, log_n, steps, warmup, seed):
     params, _, _ = setup_params(seed)
     crs = zkp.CRS.generate_from_qap(ctx, zkp.QAP(csr), zkp.SetupParams(*params), 0)
     bases = crs.pk.h_g1
-    import ctypes as C
     sc = random_fr(np.random.default_rng(seed + 7), n)
     d_sc = torch.from_numpy(sc.view(np.int64)).to(f"cuda:{ctx.device}")
 
@@ -204,7 +265,8 @@ def msm_g1_bench(zkp, ctx, log_n, steps, warmup, seed):
     return {"pairs_per_s": round(n / dt, 1), "n": n, "scalar_bits": 255, "ms_per_msm": round(dt * 1e3, 3),
             "bases": "uploaded once with 16 window-shifted copies (zk_msm_g1_upload_windows, %.0f ms)" % (t_up * 1e3),
             "plain": {"pairs_per_s": round(n / dt_plain, 1), "ms_per_msm": round(dt_plain * 1e3, 3),
-                      "bases": "uploaded once, one copy (zk_msm_g1_upload)"}}
+                      "bases": "uploaded once, one copy (zk_msm_g1_upload)"},
+            "parity": "tests/test_gpu_headline.py::test_msm_g1_2p20_closed_form (same sizes, closed form)"}
 
 
 def ntt_bench(zkp, ctx, log_n, steps, warmup, seed):
@@ -225,15 +287,20 @@ def ntt_bench(zkp, ctx, log_n, steps, warmup, seed):
         run(1)
         run(-1)
     torch.cuda.synchronize()
+    ctx.profile(True)
     t0 = time.perf_counter()
     for _ in range(steps):
         run(1)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
+    prof = ctx.profile_read()
+    ctx.profile(False)
     for _ in range(steps):
         run(-1)
     ok = bool(np.array_equal(d.cpu().numpy().view(np.uint64).reshape(-1, 4), x))
+    k = prof.get("ntt", {"ms": 0.0, "launches": 0})
     return {"log_n": log_n, "ms_per_ntt": round(dt * 1e3, 3), "elements_per_s": round(n / dt, 1),
+            "kernel_ms_per_ntt": round(k["ms"] / max(steps, 1), 4),
             "roundtrip_identity": ok}
 
 
@@ -242,10 +309,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--log-n", type=int, default=20, help="log2 constraints per GPU")
-    ap.add_argument("--cpu-log-n", type=int, default=17, help="CPU baseline sample size")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="N > 1: strong = one 2^total-log-n circuit sharded (configs[4]); weak = 2^log-n per GPU")
+    ap.add_argument("--total-log-n", type=int, default=24, help="N > 1 strong scaling: log2 constraints in total")
+    ap.add_argument("--log-n", type=int, default=20, help="log2 constraints (N = 1), per GPU (N > 1 weak)")
+    ap.add_argument("--cpu-log-n", type=int, default=17, help="single-thread CPU baseline sample size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-msm", action="store_true")
+    ap.add_argument("--no-msm", action="store_true", help="skip the configs[1] MSM and configs[2] NTT lines")
+    ap.add_argument("--no-serial", action="store_true", help="skip the serial-schedule roofline proves")
     ap.add_argument("--seed", type=int, default=0x5EED0001)
     args = ap.parse_args()
 
@@ -258,7 +329,8 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # Rehearsal knobs (not the bench contract): ZK_BENCH_DIST_BACKEND=gloo and
     # ZK_BENCH_DEVICE=0 run N ranks on one GPU with CPU-side collectives and
-    # no RCCL communicator (each rank then recomputes the whole quotient).
+    # no RCCL communicator (each rank then recomputes the whole quotient,
+    # reported as "quotient": "replicated").
     backend = os.environ.get("ZK_BENCH_DIST_BACKEND", "nccl")
     local = int(os.environ.get("ZK_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
@@ -272,27 +344,34 @@ def main():
     coll_dev = f"cuda:{local}" if backend == "nccl" else "cpu"
 
     ctx = zkp.Context(local)
-    if dist and backend == "nccl":
-        # one RCCL communicator inside the library for the distributed
-        # quotient (three all-to-alls per proof over xGMI); the unique id
-        # travels over the torch process group
-        obj = [zkp.Context.rccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        try:
+    quotient_mode = "local"
+    if dist:
+        quotient_mode = "replicated"
+        if backend == "nccl":
+            # one RCCL communicator inside the library for the distributed
+            # quotient (three all-to-alls per proof over xGMI); the unique id
+            # travels over the torch process group.  A failed attach is fatal:
+            # a replicated quotient would be a different (slower) workload.
+            obj = [zkp.Context.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
             ctx.attach_rccl(obj[0], rank, world)
-        except zkp.GrothError as e:   # every rank then recomputes the whole quotient
-            log(f"[bench] RCCL attach failed ({e}); quotient replicated per rank")
-    n = (1 << args.log_n) * world
+            quotient_mode = "distributed-rccl"
+    strong = world > 1 and args.scaling == "strong"
+    if world == 1:
+        n = 1 << args.log_n
+    elif strong:
+        n = 1 << args.total_log_n
+    else:
+        n = (1 << args.log_n) * world
     log_n_total = n.bit_length() - 1
     params, r, s = setup_params(args.seed)
-    log(f"[bench] rank0: setup 2^{log_n_total}-constraint synthetic circuit on GPU (shard {rank}/{world})")
+    log(f"[bench] setup 2^{log_n_total}-constraint synthetic circuit on GPU (shard {rank}/{world})")
     qap = zkp.QAP(zkp.CSRMatrices.synthetic(n))
     t0 = time.perf_counter()
     dpk = zkp.CRS.generate_device(ctx, qap, zkp.SetupParams(*params), 1, shard=rank, nshards=world)
     t_setup = time.perf_counter() - t0
-    z = synthetic_witness(n, args.seed + 1)
-    d_z = torch.from_numpy(z.view(np.int64)).to(f"cuda:{local}")
-    zlen = len(z)
+    d_z = ctx.synthetic_witness(n, args.seed + 1)      # identical on every rank (same seed)
+    zlen = 3 * n + 1
     log(f"[bench] setup {t_setup:.2f}s; witness ready ({zlen} vars)")
 
     def step():
@@ -325,20 +404,48 @@ def main():
         elapsed = float(t.item())
     ms_step = elapsed / args.steps * 1e3
     value = n / (elapsed / args.steps)
+    g1_pairs, g2_pairs = prove_msm_pairs(n)
 
     extra = {}
+    roofline = None
     if rank == 0 and world == 1:
-        # PCIe-inclusive rate: the witness crosses from host memory each proof
-        w = zkp.Witness(z, 1)
+        # the dominant kernel's own duration: the same proves, every kernel in
+        # order on one stream (overlap would stretch its HIP-event span)
+        serial_prof = None
+        if not args.no_serial:
+            ctx.set_schedule(3)
+            torch.cuda.synchronize()
+            ctx.profile(True)
+            t0 = time.perf_counter()
+            ks = max(3, args.steps // 2)
+            for _ in range(ks):
+                p3 = zkp.Prover.prove_device(dpk, d_z.data_ptr(), zlen, 1, r, s)
+            torch.cuda.synchronize()
+            t_ser = (time.perf_counter() - t0) / ks
+            serial_prof = ctx.profile_read()
+            ctx.profile(False)
+            ctx.set_schedule(-1)
+            if p3 != proof:
+                raise SystemExit("serial-schedule proof differs from the overlapped one")
+            extra["serial_schedule"] = {"ms_per_step": round(t_ser * 1e3, 3), "steps": ks,
+                                        "phases_ms_total": phase_table(serial_prof)}
+        roofline = roofline_from(serial_prof or prof, log_n_total, overlapped=prof)
+        # PCIe-inclusive rate (the drop-in zk_groth16_prove: witness crosses from host memory each proof)
+        z_host = d_z.cpu().numpy().view(np.uint64)
+        w = zkp.Witness(z_host, 1)
         zkp.Prover.prove(dpk, w, r=r, s=s)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(3):
-            zkp.Prover.prove(dpk, w, r=r, s=s)
+            pp = zkp.Prover.prove(dpk, w, r=r, s=s)
         torch.cuda.synchronize()
         t_pc = (time.perf_counter() - t0) / 3
+        if pp != proof:
+            raise SystemExit("host-witness proof differs from the device-witness one")
         extra["pcie_inclusive"] = {"ms_per_step": round(t_pc * 1e3, 3), "value": round(n / t_pc, 1),
-                                   "note": "zk_groth16_prove with the witness in host memory"}
+                                   "unit": "constraints/s",
+                                   "note": "zk_groth16_prove (the drop-in prove(pk, witness)): the 3n+1-element "
+                                           "witness crosses PCIe from host memory every proof"}
         dpk.free()
         if not args.no_msm:
             log("[bench] G1 MSM 2^20 (configs[1])")
@@ -346,22 +453,36 @@ def main():
             log("[bench] NTT 2^22 (configs[2])")
             extra["ntt"] = ntt_bench(zkp, ctx, 22, args.steps, args.warmup, args.seed + 31)
         if not args.no_cpu_baseline:
-            log(f"[bench] CPU baseline: oracle prove at 2^{args.cpu_log_n}, 1 thread")
-            extra["cpu_baseline"] = cpu_baseline(zkp, ctx, args.cpu_log_n, args.seed + 21)
+            log(f"[bench] CPU baseline: oracle prove at 2^{log_n_total} on all cores, 2^{args.cpu_log_n} on 1 thread")
+            extra["cpu_baseline"] = cpu_baseline(zkp, ctx, n, params, r, s, z_host, proof, args.cpu_log_n,
+                                                 args.seed + 21)
+            extra["bit_exact_vs_oracle"] = extra["cpu_baseline"]["bit_exact_vs_gpu"]
     if rank == 0:
+        if world == 1:
+            workload = f"groth16_prove_2^{log_n_total}"
+        elif strong:
+            workload = f"groth16_prove_2^{log_n_total}_sharded_{world}gpu"
+        else:
+            workload = f"groth16_prove_2^{args.log_n}_per_gpu"
         rec = {
             "metric": METRIC, "value": round(value, 1), "unit": "constraints/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "dtype": "u32", "data": "synthetic",
-            "config": {"workload": "groth16_prove", "circuit": "n x (x*y=z) (groth16-cli generate_crs)",
-                       "field": "BLS12-381 Fq/Fr Montgomery, 32x32->64-bit limb products (radix 2^28)",
-                       "constraints": n, "constraints_per_gpu": 1 << args.log_n, "num_public": 1,
-                       "parallelism": f"msm-shard{world}+quotient-a2a" if world > 1 else "single-gpu",
-                       "setup_s": round(t_setup, 2)},
-            "roofline": roofline_from(prof),
+            "config": {"workload": workload, "circuit": "n x (x*y=z) (groth16-cli generate_crs)",
+                       "field": "BLS12-381 Fq/Fr Montgomery, 32x32->64-bit limb products (radix 2^28/2^29)",
+                       "constraints": n, "constraints_per_gpu": n // world, "num_public": 1,
+                       "parallelism": (f"msm-shard{world}+quotient-a2a" if quotient_mode == "distributed-rccl"
+                                       else f"msm-shard{world}" if world > 1 else "single-gpu"),
+                       "quotient": quotient_mode, "setup_s": round(t_setup, 2)},
+            "msm_pairs_per_s": {"g1": round(g1_pairs / (ms_step / 1e3), 1), "g2": round(g2_pairs / (ms_step / 1e3), 1),
+                                "total": round((g1_pairs + g2_pairs) / (ms_step / 1e3), 1),
+                                "note": "scalar-point pairs of the reference's 5 MSMs per proof (G1 10n+6, G2 3n+3) "
+                                        "/ whole-job time per proof"},
+            "roofline": roofline,
             "phases_ms_total": phase_table(prof),
-            "proof_compressed_prefix": proof.serialize_compressed().hex()[:32],
+            "proof_compressed": proof.serialize_compressed().hex(),
+            "build_id": zkp.build_id(),
         }
         rec.update(extra)
         rec.setdefault("cpu_baseline", None)

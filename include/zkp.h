@@ -41,7 +41,9 @@ typedef enum {
   ZK_ERR_SETUP_PARAMS = 5,
   ZK_ERR_DEVICE = 6,
   ZK_ERR_RCCL = 7,
-  ZK_ERR_ARG = 8
+  ZK_ERR_ARG = 8,          /* bad argument: NULL, out of range, non-canonical field element */
+  ZK_ERR_DIMENSION = 9     /* FieldError::DimensionMismatch (crates/groth16-field/src/lib.rs:127-129),
+                              as returned by QAP::evaluate_at (crates/groth16-qap/src/lib.rs:190-198) */
 } zk_status;
 
 typedef struct { uint64_t l[4]; } zk_fr;                                   /* 32 B  */
@@ -111,13 +113,29 @@ int zk_ctx_profile_read(zk_ctx *ctx, char *names, size_t names_cap, double *ms,
                         uint64_t *launches, uint64_t *units, size_t max_phases,
                         size_t *nphases);
 
+/* Build provenance: "<git HEAD>[-dirty] src:<16 hex of sha256 over the
+ * sources in zero-knowledge-proofs_amd/csrc/ *.hip and *.hpp (sorted) and
+ * include/zkp.h>".  __graft_entry__.smoke() recomputes the source hash from
+ * the tree it runs in and refuses a library built from other sources.  No
+ * reference counterpart. */
+const char *zk_build_id(void);
+/* Prove stream schedule (measurement): -1 default (ZK_PROVE_SCHED or the
+ * overlapped four-stream schedule), 0 overlapped, 1 G2 after the quotient,
+ * 3 every kernel in order on one stream (isolated kernel durations), 4
+ * quotient queued first.  Results never depend on it.  No reference
+ * counterpart. */
+int zk_ctx_set_schedule(zk_ctx *ctx, int schedule);
+
 /* ---------------------------------------------------------------- MSM --- */
 /* Sum_i scalars[i] * bases[i], normalised to affine.  Replaces
  * Prover::multi_scalar_mult_g1 -> G1Projective::msm (ark-ec 0.4.2
  * VariableBaseMSM::msm), crates/groth16-core/src/lib.rs:275-286.
  * nbases != nscalars -> ZK_ERR_MSM_LEN (ark's Err(min_len)).
  * scalar_bits: 64 when every scalar is < 2^64 (the prove path's lo64
- * scalars), else 255.  Infinity bases and zero scalars are allowed. */
+ * scalars), else 255.  Infinity bases and zero scalars are allowed.
+ * A scalar >= r (ark's Fr is always reduced) or wider than scalar_bits is
+ * ZK_ERR_ARG -- checked on the host for host scalars, by a device flag for
+ * the *_dev entry points. */
 int zk_msm_g1(zk_ctx *ctx, const zk_g1_affine *bases, size_t nbases,
               const zk_fr *scalars, size_t nscalars, uint32_t scalar_bits,
               zk_g1_affine *out);
@@ -171,7 +189,14 @@ int zk_groth16_setup_dev(zk_ctx *ctx, const zk_r1cs_csr *qap, const zk_setup_par
                          uint64_t num_public, zk_pk_dev **pk_out, zk_vk *vk);
 
 /* -------------------------------------------------------------- prove --- */
-/* Upload a proving key + its constraint system once; it stays resident. */
+/* Upload a proving key + its constraint system once; it stays resident.
+ * The CSR is required because the reference's ProvingKey embeds the QAP as
+ * dense per-variable polynomials (pk.qap, crates/groth16-setup/src/lib.rs:51,
+ * built by QAP::from_r1cs, crates/groth16-qap/src/lib.rs:143-170): a Rust
+ * caller passes the R1CS it built the QAP from (its A/B/C rows, the same
+ * matrices the polynomials interpolate) instead of those polynomials, which
+ * are infeasible beyond ~2^12 constraints.  This is the one
+ * change to the drop-in contract of prove(pk, witness, rng). */
 int zk_pk_upload(zk_ctx *ctx, const zk_pk *pk, const zk_r1cs_csr *qap, zk_pk_dev **out);
 void zk_pk_free(zk_pk_dev *pk);
 
@@ -179,7 +204,8 @@ void zk_pk_free(zk_pk_dev *pk);
  * z = full assignment [1 | public | witness] (Witness::assignment), zlen its
  * length, num_public = Witness::num_public.  r and s are the two Fr::rand
  * draws of core:152-153, made explicit so proofs are reproducible.
- * Errors: ZK_ERR_INVALID_WITNESS (Witness::new / validate), ZK_ERR_QAP_DIVISION. */
+ * Errors: ZK_ERR_INVALID_WITNESS (Witness::new / validate), ZK_ERR_QAP_DIVISION;
+ * ZK_ERR_ARG when r, s or some z_i is >= r (a device flag over z). */
 int zk_groth16_prove(zk_ctx *ctx, const zk_pk_dev *pk, const zk_fr *z, size_t zlen,
                      size_t num_public, const zk_fr *r, const zk_fr *s, zk_proof *out);
 /* Same with z in DEVICE memory (zlen canonical zk_fr). */
@@ -220,6 +246,27 @@ int zk_ctx_attach_rccl(zk_ctx *ctx, const uint8_t unique_id[128], int rank, int 
 int zk_test_prove_virtual_shards(zk_ctx *ctx, const zk_pk_dev *const *shards, uint32_t nshards,
                                  const void *d_z, size_t zlen, size_t num_public, const zk_fr *r,
                                  const zk_fr *s, zk_proof *out);
+
+/* ---------------------------------------------------------------- QAP --- */
+/* QAP::evaluate_at (crates/groth16-qap/src/lib.rs:190-220): out[0..2] =
+ * A(point), B(point), C(point) = sum_i z_i A_i(point) etc., out[3] = Z(point)
+ * = point^n - 1, from the sparse matrices (sum_j (Az)_j L_j(point) with the
+ * domain's Lagrange basis -- the value the dense interpolants give).
+ * zlen != num_variables -> ZK_ERR_DIMENSION (FieldError::DimensionMismatch).
+ * QAP::verify_evaluation (qap:274-282) is a*b == c on these values. */
+int zk_qap_evaluate_at(zk_ctx *ctx, const zk_r1cs_csr *qap, const zk_fr *point, const zk_fr *z, size_t zlen,
+                       zk_fr out[4]);
+/* utils::batch_evaluate (crates/groth16-qap/src/lib.rs:315-322): out[p] =
+ * poly_p(point) for npolys dense polynomials in coefficient form, poly p's
+ * coefficients (lowest degree first) at coeffs[offsets[p] .. offsets[p+1]). */
+int zk_poly_evaluate_batch(zk_ctx *ctx, const zk_fr *coeffs, const uint64_t *offsets, size_t npolys,
+                           const zk_fr *point, zk_fr *out);
+
+/* Synthetic data for benchmarks: the witness of the groth16-cli circuit
+ * n x (x*y = z) (crates/groth16-cli/src/lib.rs:57-70), z = [1, x_0, y_0,
+ * x_0 y_0, ...], 3n+1 canonical zk_fr written to DEVICE memory d_z, with
+ * x_j, y_j < 2^254 drawn from a counter-based splitmix64 stream of `seed`. */
+int zk_synthetic_witness_dev(zk_ctx *ctx, uint64_t n, uint64_t seed, void *d_z);
 
 /* ------------------------------------------------------ serialization --- */
 /* ark-serialize CanonicalSerialize, compressed (zcash flag bits), for

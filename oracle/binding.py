@@ -55,8 +55,35 @@ def lib():
         L.or_init()
         L.or_domain_size.restype = C.c_uint64
         L.or_splitmix64.restype = C.c_uint64
+        L.or_set_threads(C.c_int(default_threads()))
         _lib = L
     return _lib
+
+
+def default_threads():
+    """ZK_ORACLE_THREADS, else OMP_NUM_THREADS (16 on the GPU box), else
+    min(16, cpu_count): the oracle is a checker, parallel by default."""
+    for k in ("ZK_ORACLE_THREADS", "OMP_NUM_THREADS"):
+        if os.environ.get(k, "").isdigit():
+            return max(1, int(os.environ[k]))
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def set_threads(n):
+    """1 = the reference's single-threaded arkworks build (Cargo.lock:101-113)."""
+    lib().or_set_threads(C.c_int(int(n)))
+
+
+def get_threads():
+    return int(lib().or_get_threads())
+
+
+def g1_lin_bases(a, b, n):
+    """(a + i b) G1 for i < n, (n, 13) words."""
+    out = np.zeros((n, 13), dtype=np.uint64)
+    lib().or_g1_lin_bases(_p(out), _p(np.array(int_to_limbs(a, 4), dtype=np.uint64)),
+                          _p(np.array(int_to_limbs(b, 4), dtype=np.uint64)), C.c_uint64(n))
+    return out
 
 
 def _p(a):

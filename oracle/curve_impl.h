@@ -166,7 +166,7 @@ static void G(mul_bits)(G(jac) *o, const G(jac) *p, const uint64_t *k, int nbits
  * builds ark-ec without the `parallel` feature, Cargo.lock:101-113).
  * scalars: canonical 4-limb integers.
  */
-static void G(msm_ark)(G(jac) *out, const G(aff) *bases, const uint64_t *scalars, size_t n) {
+static void G(msm_ark_serial)(G(jac) *out, const G(aff) *bases, const uint64_t *scalars, size_t n) {
   G(set_inf)(out);
   if (n == 0) return;
   int c = n < 32 ? 3 : (int)(ark_log2(n) * 69 / 100) + 2;
@@ -201,6 +201,41 @@ static void G(msm_ark)(G(jac) *out, const G(aff) *bases, const uint64_t *scalars
   }
   G(add)(out, &wsum[0], &tot);
   free(dig); free(bk); free(wsum);
+}
+
+/*
+ * The MSM the oracle runs.  With g_nthreads == 1 it IS msm_ark_serial (the
+ * reference's single-threaded arkworks build).  With more threads the points
+ * are cut into g_nthreads contiguous chunks, each chunk runs the same serial
+ * algorithm (its own window size) and the chunk sums are added in order --
+ * the result is the same group element, so the affine output is unchanged.
+ * Chunks below 4096 points are not worth a thread.
+ */
+static void G(msm_ark)(G(jac) *out, const G(aff) *bases, const uint64_t *scalars, size_t n) {
+  int T = g_nthreads;
+  if (T > 1 && n / (size_t)T < 4096) T = (int)(n / 4096);
+  if (T <= 1) { G(msm_ark_serial)(out, bases, scalars, n); return; }
+  G(jac) *part = (G(jac) *)malloc(sizeof(G(jac)) * (size_t)T);
+#pragma omp parallel for schedule(dynamic, 1) num_threads(T)
+  for (int t = 0; t < T; t++) {
+    size_t lo = n * (size_t)t / (size_t)T, hi = n * (size_t)(t + 1) / (size_t)T;
+    G(msm_ark_serial)(&part[t], bases + lo, scalars + 4 * lo, hi - lo);
+  }
+  G(set_inf)(out);
+  for (int t = 0; t < T; t++) G(add)(out, out, &part[t]);
+  free(part);
+}
+
+/* Jacobian -> affine for n points, batch-inverted in g_nthreads chunks. */
+static void G(batch_to_aff_par)(G(aff) *o, const G(jac) *p, size_t n) {
+  int T = g_nthreads;
+  if (T > 1 && n / (size_t)T < 1024) T = (int)(n / 1024);
+  if (T <= 1) { G(batch_to_aff)(o, p, n); return; }
+#pragma omp parallel for schedule(static) num_threads(T)
+  for (int t = 0; t < T; t++) {
+    size_t lo = n * (size_t)t / (size_t)T, hi = n * (size_t)(t + 1) / (size_t)T;
+    G(batch_to_aff)(o + lo, p + lo, hi - lo);
+  }
 }
 
 /* fixed-base table: 8-bit windows over a 64-bit scalar, tab[w*256 + d] = d*2^(8w)*P */

@@ -159,6 +159,15 @@ static void fq2_inv(fq2 *o, const fq2 *a) {
   fq_mul(&t1, &a->c1, &n); fq_neg(&o->c1, &t1);
 }
 
+/* OpenMP threads for the MSM chunks, FFT butterflies and point loads.
+ * 1 = the reference's single-threaded arkworks build (Cargo.lock:101-113,
+ * 161-170: no `parallel` feature); or_set_threads raises it for tests and
+ * the all-core CPU baseline.  Results never depend on it. */
+static int g_nthreads = 1;
+void or_set_threads(int n) { g_nthreads = n > 0 ? n : 1; }
+int or_get_threads(void) { return g_nthreads; }
+#define OMP_T(n, min_per) (g_nthreads > 1 && (n) >= (u64)(min_per) * 2 ? g_nthreads : 1)
+
 /* ark_std::log2: exact for powers of two, else ceil */
 static u64 ark_log2(u64 x) {
   if (x <= 1) return 0;
@@ -327,6 +336,33 @@ void or_g2_mul(u64 out[25], const u64 p[25], const u64 k[4]) {
   g2_aff a; g2_jac j; g2_load(&a, p); g2_from_aff(&j, &a); g2_mul_bits(&j, &j, k, 256); g2_to_aff(&a, &j); g2_store(out, &a);
 }
 
+/* bases[i] = (a + i b) G1 for i < n (the closed-form MSM KAT of SURVEY
+ * 8(d): sum_i s_i bases[i] = (a sum s_i + b sum i s_i) G1).  Each of
+ * g_nthreads chunks starts from (a + lo b) G1 and steps by b G1; one batch
+ * inversion per chunk. */
+void or_g1_lin_bases(u64 *out, const u64 a[4], const u64 b[4], u64 n) {
+  if (n == 0) return;
+  fr am, bm; fr_to_mont(&am, a); fr_to_mont(&bm, b);
+  g1_jac gj; g1_from_aff(&gj, &G1_GEN);
+  g1_jac bj; g1_aff bstep;
+  g1_mul_bits(&bj, &gj, b, 256); g1_to_aff(&bstep, &bj);
+  int T = OMP_T(n, 4096);
+#pragma omp parallel for schedule(static) num_threads(T)
+  for (int t = 0; t < T; t++) {
+    u64 lo = n * (u64)t / (u64)T, hi = n * (u64)(t + 1) / (u64)T;
+    if (lo >= hi) continue;
+    fr k, lo_m; fr_from_u64(&lo_m, lo); fr_mul(&k, &lo_m, &bm); fr_add(&k, &k, &am);
+    u64 kc[4]; fr_from_mont(kc, &k);
+    g1_jac *J = (g1_jac *)malloc(sizeof(g1_jac) * (hi - lo));
+    g1_aff *A = (g1_aff *)malloc(sizeof(g1_aff) * (hi - lo));
+    g1_jac p; g1_mul_bits(&p, &gj, kc, 256);
+    for (u64 i = lo; i < hi; i++) { J[i - lo] = p; g1_madd(&p, &p, &bstep); }
+    g1_batch_to_aff(A, J, hi - lo);
+    for (u64 i = lo; i < hi; i++) g1_store(out + 13 * i, &A[i - lo]);
+    free(J); free(A);
+  }
+}
+
 /* zcash / ark-bls12-381 0.4 compressed encoding: big-endian x with flags in the
  * top bits of byte 0: 0x80 compressed, 0x40 infinity, 0x20 y lexicographically
  * largest (y > (p-1)/2; for Fq2 compare c1 first, then c0). */
@@ -378,38 +414,63 @@ int or_msm_g2(u64 out[25], const u64 *bases, const u64 *scalars, u64 n) {
 /* ------------------------------------------------------------------------ */
 /* FFT (ark-poly Radix2EvaluationDomain semantics, natural order in/out)    */
 /* ------------------------------------------------------------------------ */
+/* tw[k] = w^k for k < m, in chunks that start from w^lo */
+static void pow_table(fr *tw, const fr *w, u64 m) {
+  int T = OMP_T(m, 4096);
+#pragma omp parallel for schedule(static) num_threads(T)
+  for (int t = 0; t < T; t++) {
+    u64 lo = m * (u64)t / (u64)T, hi = m * (u64)(t + 1) / (u64)T;
+    if (lo >= hi) continue;
+    u64 e[1] = {lo};
+    fr p; fr_pow(&p, w, e, 1);
+    for (u64 k = lo; k < hi; k++) { tw[k] = p; fr_mul(&p, &p, w); }
+  }
+}
+static inline u64 bitrev(u64 x, uint32_t bits) {
+  u64 r = 0;
+  for (uint32_t i = 0; i < bits; i++) { r = (r << 1) | (x & 1); x >>= 1; }
+  return r;
+}
 static void fft_mont(fr *a, uint32_t log_n, int inverse) {
   u64 n = 1ULL << log_n;
-  for (u64 i = 1, j = 0; i < n; i++) {           /* bit reversal */
-    u64 bit = n >> 1;
-    for (; j & bit; bit >>= 1) j ^= bit;
-    j ^= bit;
-    if (i < j) { fr t = a[i]; a[i] = a[j]; a[j] = t; }
+  int T = OMP_T(n, 4096);
+#pragma omp parallel for schedule(static) num_threads(T)
+  for (long long i = 0; i < (long long)n; i++) {      /* bit reversal */
+    u64 j = bitrev((u64)i, log_n);
+    if ((u64)i < j) { fr t = a[i]; a[i] = a[j]; a[j] = t; }
   }
+  fr *tw = (fr *)malloc(sizeof(fr) * (n > 1 ? n / 2 : 1));
   for (uint32_t s = 1; s <= log_n; s++) {
     u64 len = 1ULL << s, half = len >> 1;
     fr wl; fr_root(&wl, s);
     if (inverse) fr_inv(&wl, &wl);
-    fr *tw = (fr *)malloc(sizeof(fr) * half);
-    tw[0] = FR_ONE;
-    for (u64 k = 1; k < half; k++) fr_mul(&tw[k], &tw[k - 1], &wl);
-    for (u64 i = 0; i < n; i += len)
-      for (u64 k = 0; k < half; k++) {
-        fr u = a[i + k], v;
-        fr_mul(&v, &a[i + k + half], &tw[k]);
-        fr_add(&a[i + k], &u, &v);
-        fr_sub(&a[i + k + half], &u, &v);
-      }
-    free(tw);
+    pow_table(tw, &wl, half);
+#pragma omp parallel for schedule(static) num_threads(T)
+    for (long long b = 0; b < (long long)(n / 2); b++) {
+      u64 k = (u64)b & (half - 1), i = ((u64)b >> (s - 1)) * len + k;
+      fr u = a[i], v;
+      fr_mul(&v, &a[i + half], &tw[k]);
+      fr_add(&a[i], &u, &v);
+      fr_sub(&a[i + half], &u, &v);
+    }
   }
+  free(tw);
   if (inverse) {
     fr ninv; fr_from_u64(&ninv, n); fr_inv(&ninv, &ninv);
-    for (u64 i = 0; i < n; i++) fr_mul(&a[i], &a[i], &ninv);
+#pragma omp parallel for schedule(static) num_threads(T)
+    for (long long i = 0; i < (long long)n; i++) fr_mul(&a[i], &a[i], &ninv);
   }
 }
 static void coset_scale(fr *a, u64 n, const fr *g) {
-  fr p = FR_ONE;
-  for (u64 i = 0; i < n; i++) { fr_mul(&a[i], &a[i], &p); fr_mul(&p, &p, g); }
+  int T = OMP_T(n, 4096);
+#pragma omp parallel for schedule(static) num_threads(T)
+  for (int t = 0; t < T; t++) {
+    u64 lo = n * (u64)t / (u64)T, hi = n * (u64)(t + 1) / (u64)T;
+    if (lo >= hi) continue;
+    u64 e[1] = {lo};
+    fr p; fr_pow(&p, g, e, 1);
+    for (u64 i = lo; i < hi; i++) { fr_mul(&a[i], &a[i], &p); fr_mul(&p, &p, g); }
+  }
 }
 
 void or_fft(u64 *data, uint32_t log_n, int inverse) {
@@ -461,7 +522,8 @@ static void csr_row_dot(fr *o, const u64 *rp, const uint32_t *col, const u64 *va
 
 static fr *load_z(const u64 *z, u64 V) {
   fr *zm = (fr *)malloc(sizeof(fr) * (V ? V : 1));
-  for (u64 i = 0; i < V; i++) fr_to_mont(&zm[i], z + 4 * i);
+#pragma omp parallel for schedule(static) num_threads(OMP_T(V, 4096))
+  for (long long i = 0; i < (long long)V; i++) fr_to_mont(&zm[i], z + 4 * i);
   return zm;
 }
 
@@ -487,7 +549,9 @@ static int quotient_mont(const or_r1cs *cs, const fr *zm, u64 V, fr *h) {
   uint32_t ln = log2_exact(n);
   fr *a = (fr *)calloc(n, sizeof(fr)), *b = (fr *)calloc(n, sizeof(fr)), *c = (fr *)calloc(n, sizeof(fr));
   int bad = 0;
-  for (u64 j = 0; j < nc; j++) {
+#pragma omp parallel for schedule(static) reduction(| : bad) num_threads(OMP_T(nc, 4096))
+  for (long long jj = 0; jj < (long long)nc; jj++) {
+    u64 j = (u64)jj;
     csr_row_dot(&a[j], cs->a_rowptr, cs->a_col, cs->a_val, j, zm, V);
     csr_row_dot(&b[j], cs->b_rowptr, cs->b_col, cs->b_val, j, zm, V);
     csr_row_dot(&c[j], cs->c_rowptr, cs->c_col, cs->c_val, j, zm, V);
@@ -505,7 +569,8 @@ static int quotient_mont(const or_r1cs *cs, const fr *zm, u64 V, fr *h) {
   fr gn = FR_ONE, zinv;
   for (u64 i = 0; i < n; i++) fr_mul(&gn, &gn, &FR_GEN);
   fr_sub(&zinv, &gn, &FR_ONE); fr_inv(&zinv, &zinv);
-  for (u64 i = 0; i < n; i++) {
+#pragma omp parallel for schedule(static) num_threads(OMP_T(n, 4096))
+  for (long long i = 0; i < (long long)n; i++) {
     fr t; fr_mul(&t, &a[i], &b[i]); fr_sub(&t, &t, &c[i]); fr_mul(&h[i], &t, &zinv);
   }
   fft_mont(h, ln, 1);
@@ -716,6 +781,37 @@ typedef struct { u64 *sc; g1_aff *pt; u64 n; } g1_terms;
 typedef struct { u64 *sc; g2_aff *pt; u64 n; } g2_terms;
 static void t1_push(g1_terms *t, const u64 *s, const g1_aff *p) { memcpy(t->sc + 4 * t->n, s, 32); t->pt[t->n++] = *p; }
 static void t2_push(g2_terms *t, const u64 *s, const g2_aff *p) { memcpy(t->sc + 4 * t->n, s, 32); t->pt[t->n++] = *p; }
+/* Append the terms (w_i, bases[i - off]) for lo <= i < hi with w_i != 0 and
+ * i - off < len, in index order (the filter of core:169-175 / 187-193 /
+ * 226-233 / 250-252); the selection is one sequential pass, the Montgomery
+ * loads of the selected points run on g_nthreads threads. */
+static u64 *g_sel;                                   /* scratch: selected indices */
+static u64 select_terms(const u64 *w, u64 lo, u64 hi, u64 off, u64 len) {
+  u64 m = 0;
+  for (u64 i = lo; i < hi; i++)
+    if (w[4 * i] && i - off < len) g_sel[m++] = i;
+  return m;
+}
+static void t1_append(g1_terms *t, const u64 *w, u64 lo, u64 hi, const u64 *bases, u64 off, u64 len) {
+  u64 m = select_terms(w, lo, hi, off, len), base = t->n;
+#pragma omp parallel for schedule(static) num_threads(OMP_T(m, 4096))
+  for (long long j = 0; j < (long long)m; j++) {
+    u64 i = g_sel[j];
+    memcpy(t->sc + 4 * (base + (u64)j), w + 4 * i, 32);
+    g1_load(&t->pt[base + (u64)j], bases + 13 * (i - off));
+  }
+  t->n += m;
+}
+static void t2_append(g2_terms *t, const u64 *w, u64 lo, u64 hi, const u64 *bases, u64 off, u64 len) {
+  u64 m = select_terms(w, lo, hi, off, len), base = t->n;
+#pragma omp parallel for schedule(static) num_threads(OMP_T(m, 4096))
+  for (long long j = 0; j < (long long)m; j++) {
+    u64 i = g_sel[j];
+    memcpy(t->sc + 4 * (base + (u64)j), w + 4 * i, 32);
+    g2_load(&t->pt[base + (u64)j], bases + 25 * (i - off));
+  }
+  t->n += m;
+}
 /* multi_scalar_mult_g1 (core:275-286): empty -> identity, else msm().into_affine() */
 static void msm1(g1_aff *o, const g1_terms *t) { g1_jac j; g1_msm_ark(&j, t->pt, t->sc, t->n); g1_to_aff(o, &j); }
 static void msm2(g2_aff *o, const g2_terms *t) { g2_jac j; g2_msm_ark(&j, t->pt, t->sc, t->n); g2_to_aff(o, &j); }
@@ -734,23 +830,23 @@ int or_prove(const or_pk *pk, const or_r1cs *cs, const u64 *z, u64 zlen, u64 num
   u64 *w = (u64 *)malloc(sizeof(u64) * 4 * V);
   for (u64 i = 0; i < V; i++) { w[4 * i] = z[4 * i]; w[4 * i + 1] = w[4 * i + 2] = w[4 * i + 3] = 0; }
   u64 cap = V + n + 8;
+  g_sel = (u64 *)malloc(sizeof(u64) * (V > n ? V : n));
   g1_terms T1 = {(u64 *)malloc(32 * cap), (g1_aff *)malloc(sizeof(g1_aff) * cap), 0};
   g2_terms T2 = {(u64 *)malloc(32 * (V + 4)), (g2_aff *)malloc(sizeof(g2_aff) * (V + 4)), 0};
   g1_aff P, pi_a, pi_c, h1, b1; g2_aff Q, pi_b;
+  u64 *hw = NULL;
 
   /* pi_A (core:164-179) */
   T1.n = 0;
   g1_load(&P, pk->alpha_g1); t1_push(&T1, one, &P);
-  for (u64 i = 0; i < V; i++)
-    if (w[4 * i] && i < pk->a_len) { g1_load(&P, pk->a_g1 + 13 * i); t1_push(&T1, w + 4 * i, &P); }
+  t1_append(&T1, w, 0, V, pk->a_g1, 0, pk->a_len);
   g1_load(&P, pk->delta_g1); t1_push(&T1, r, &P);
   msm1(&pi_a, &T1);
 
   /* pi_B (core:182-197) */
   T2.n = 0;
   g2_load(&Q, pk->beta_g2); t2_push(&T2, one, &Q);
-  for (u64 i = 0; i < V; i++)
-    if (w[4 * i] && i < pk->b2_len) { g2_load(&Q, pk->b_g2 + 25 * i); t2_push(&T2, w + 4 * i, &Q); }
+  t2_append(&T2, w, 0, V, pk->b_g2, 0, pk->b2_len);
   g2_load(&Q, pk->delta_g2); t2_push(&T2, s, &Q);
   msm2(&pi_b, &T2);
 
@@ -760,27 +856,24 @@ int or_prove(const or_pk *pk, const or_r1cs *cs, const u64 *z, u64 zlen, u64 num
   rc = quotient_mont(cs, zm, V, h);
   free(zm);
   if (rc) goto done;
+  /* h_coeffs = lo64 (core:203-208), zipped with h_g1 (core:211-219) */
+  hw = (u64 *)calloc(4 * n, sizeof(u64));
+#pragma omp parallel for schedule(static) num_threads(OMP_T(n, 4096))
+  for (long long i = 0; i < (long long)n; i++) hw[4 * i] = fr_lo64(&h[i]);
   T1.n = 0;
-  for (u64 i = 0; i < n && i < pk->h_len; i++) {
-    u64 hc[4] = {fr_lo64(&h[i]), 0, 0, 0};
-    if (hc[0]) { g1_load(&P, pk->h_g1 + 13 * i); t1_push(&T1, hc, &P); }
-  }
+  t1_append(&T1, hw, 0, n, pk->h_g1, 0, pk->h_len);
   if (T1.n == 0) { h1.inf = 1; fq_set_zero(&h1.x); fq_set_zero(&h1.y); }
   else msm1(&h1, &T1);
 
   /* B1 (core:246-255) */
   T1.n = 0;
   g1_load(&P, pk->beta_g1); t1_push(&T1, one, &P);
-  for (u64 i = 0; i < V; i++)
-    if (w[4 * i] && i < pk->b_len) { g1_load(&P, pk->b_g1 + 13 * i); t1_push(&T1, w + 4 * i, &P); }
+  t1_append(&T1, w, 0, V, pk->b_g1, 0, pk->b_len);
   msm1(&b1, &T1);
 
   /* pi_C (core:224-265) */
   T1.n = 0;
-  for (u64 i = pk->num_public + 1; i < V; i++)
-    if (w[4 * i] && (i - pk->num_public - 1) < pk->ic_len) {
-      g1_load(&P, pk->ic_g1 + 13 * (i - pk->num_public - 1)); t1_push(&T1, w + 4 * i, &P);
-    }
+  t1_append(&T1, w, pk->num_public + 1, V, pk->ic_g1, pk->num_public + 1, pk->ic_len);
   if (!h1.inf) t1_push(&T1, one, &h1);
   if (!pi_a.inf) t1_push(&T1, s, &pi_a);
   if (!b1.inf) t1_push(&T1, r, &b1);
@@ -791,7 +884,8 @@ int or_prove(const or_pk *pk, const or_r1cs *cs, const u64 *z, u64 zlen, u64 num
   g2_store(proof + 13, &pi_b);
   g1_store(proof + 38, &pi_c);
 done:
-  free(w); free(h); free(T1.sc); free(T1.pt); free(T2.sc); free(T2.pt);
+  free(w); free(h); free(hw); free(g_sel); g_sel = NULL;
+  free(T1.sc); free(T1.pt); free(T2.sc); free(T2.pt);
   return rc;
 }
 

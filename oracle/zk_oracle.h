@@ -108,7 +108,15 @@ void or_g2_mul(uint64_t out[25], const uint64_t p[25], const uint64_t k[4]);
 void or_g1_compress(uint8_t out[48], const uint64_t p[13]);
 void or_g2_compress(uint8_t out[96], const uint64_t p[25]);
 
-/* ---- MSM: ark-ec 0.4 msm_bigint_wnaf restated (single thread) ---- */
+/* ---- threads: 1 (default) = the reference's single-threaded arkworks build;
+ * more run the MSM over contiguous point chunks and the FFT butterflies /
+ * point loads in parallel (OpenMP).  Outputs never depend on it. ---- */
+void or_set_threads(int n);
+int  or_get_threads(void);
+/* bases[i] = (a + i b) G1, i < n (13 words each): closed-form MSM KAT */
+void or_g1_lin_bases(uint64_t *out, const uint64_t a[4], const uint64_t b[4], uint64_t n);
+
+/* ---- MSM: ark-ec 0.4 msm_bigint_wnaf restated (chunked over threads) ---- */
 int or_msm_g1(uint64_t out[13], const uint64_t *bases, const uint64_t *scalars, uint64_t n);
 int or_msm_g2(uint64_t out[25], const uint64_t *bases, const uint64_t *scalars, uint64_t n);
 

@@ -47,3 +47,20 @@ def qap_from_case(zkp, case):
     for a, b, c in constraints_of(case):
         cs.enforce_multiplication(zkp.LinearCombination(a), zkp.LinearCombination(b), zkp.LinearCombination(c))
     return zkp.QAP.from_r1cs(cs)
+
+
+def oracle_pk_from(oracle, pk):
+    """The oracle's PK struct holding the same bases as a product ProvingKey
+    (host arrays, canonical words) -- the checker proves from the same key."""
+    V, n = pk.qap.num_variables, pk.qap.domain_size
+    opk = oracle.PK(V, n, pk.num_public)
+    for nm in ("a_g1", "b_g1", "b_g2", "h_g1"):
+        getattr(opk, nm)[:] = getattr(pk, nm)
+    opk.ic_g1[:len(pk.ic_g1)] = pk.ic_g1
+    for nm in ("alpha_g1", "beta_g1", "delta_g1", "beta_g2", "delta_g2"):
+        arr = getattr(opk.s, nm)
+        for i, x in enumerate(pk.point(nm)):
+            arr[i] = int(x)
+    opk.s.a_len, opk.s.b_len, opk.s.b2_len = len(pk.a_g1), len(pk.b_g1), len(pk.b_g2)
+    opk.s.ic_len, opk.s.h_len, opk.s.num_public = len(pk.ic_g1), len(pk.h_g1), pk.num_public
+    return opk

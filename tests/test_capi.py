@@ -47,3 +47,11 @@ def test_ctx_create_fails_cleanly_without_gpu(zkp):
 
 def test_combine_rejects_bad_args(zkp):
     assert zkp.lib().zk_groth16_prove_combine(None, 0, None, None, None) == zkp.ZK_ERR_ARG
+
+
+def test_build_id_matches_sources(zkp):
+    """libzkp_amd.so embeds the hash of the sources it was compiled from
+    (Makefile -> zk_build_id); it must be this tree's."""
+    bid = zkp.build_id()
+    assert " src:" in bid
+    assert bid.endswith("src:" + zkp.source_hash()), (bid, zkp.source_hash())

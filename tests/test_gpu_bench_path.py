@@ -1,0 +1,52 @@
+"""bench.py's N > 1 path (the configs[4] strong-scaling line) rehearsed on ONE
+GPU: two torchrun ranks on device 0 with gloo collectives
+(ZK_BENCH_DIST_BACKEND=gloo ZK_BENCH_DEVICE=0; no RCCL communicator, so each
+rank recomputes the quotient -- the line says "quotient": "replicated").  The
+folded proof of the sharded run must equal the single-GPU proof of the same
+circuit, key parameters, witness and r, s byte for byte."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_rank_path_matches_single_gpu(ctx, zkp):
+    log_n, seed = 12, 0x5EED0001
+    env = dict(os.environ, ZK_BENCH_DIST_BACKEND="gloo", ZK_BENCH_DEVICE="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+           "--total-log-n", str(log_n), "--seed", str(seed)]
+    res = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert res.returncode == 0, res.stderr[-3000:]
+    line = [ln for ln in res.stdout.splitlines() if ln.startswith("{")][-1]
+    rec = json.loads(line)
+    assert rec["n_gpus"] == 2 and rec["scaling"] == "strong"
+    assert rec["config"]["constraints"] == 1 << log_n and rec["config"]["quotient"] == "replicated"
+    sys.path.insert(0, ROOT)
+    import bench
+    params, r, s = bench.setup_params(seed)
+    n = 1 << log_n
+    qap = zkp.QAP(zkp.CSRMatrices.synthetic(n))
+    dpk = zkp.CRS.generate_device(ctx, qap, zkp.SetupParams(*params), 1)
+    z = ctx.synthetic_witness(n, seed + 1)
+    proof = zkp.Prover.prove_device(dpk, z.data_ptr(), 3 * n + 1, 1, r, s)
+    dpk.free()
+    assert rec["proof_compressed"] == proof.serialize_compressed().hex()
+    del np

@@ -145,3 +145,39 @@ def test_oracle_msm_linearity(oracle):
     s = oracle.fr_ints(sc)
     k = (a * sum(s) + b * sum(i * x for i, x in enumerate(s))) % R
     assert np.array_equal(oracle.msm_g1(np.array(bases), sc), oracle.g1_mul(g, k))
+
+
+def test_oracle_threads_do_not_change_results(oracle, pyref):
+    """The chunked multi-thread oracle (MSM chunks, FFT butterflies, parallel
+    point loads) gives the single-thread restatement's outputs bit for bit:
+    MSM over G1 and G2, the FFT, the 2^13 prove, and the chunked (a + i b) G1
+    bases against the incremental chain."""
+    saved = oracle.get_threads()
+    try:
+        n = 1 << 13
+        csr = oracle.CSR.synthetic(n)
+        rng = pyref.SplitMix64(0x7E)
+        params = [rng.fr() for _ in range(5)]
+        r, s = rng.fr(), rng.fr()
+        rc, pk, _ = oracle.setup(csr, params, 1, nthreads=8)
+        z = oracle.synthetic_witness(n, 0x7F)
+        bases = oracle.g1_lin_bases(0xABC, 0xDEF, 1 << 14)
+        sc = oracle.random_fr(1 << 14, 0x80)
+        x = oracle.random_fr(1 << 14, 0x81)
+        out = {}
+        for t in (1, 8):
+            oracle.set_threads(t)
+            out[t] = (oracle.prove(pk, csr, z, 1, r, s), oracle.msm_g1(bases, sc),
+                      oracle.msm_g2(pk.b_g2[:9000], sc[:9000]), oracle.fft(x), oracle.g1_lin_bases(0xABC, 0xDEF, 1 << 14))
+        assert out[1][0][0] == out[8][0][0] == oracle.OR_OK
+        assert np.array_equal(out[1][0][1], out[8][0][1])
+        for k in range(1, 5):
+            assert np.array_equal(out[1][k], out[8][k])
+        g = oracle.g1_generator()
+        step, p = oracle.g1_mul(g, 0xDEF), oracle.g1_mul(g, 0xABC)
+        for i in range(1, 6000):
+            p = oracle.g1_add(p, step)
+            if i in (1, 4095, 4096, 5999):
+                assert np.array_equal(bases[i], p)
+    finally:
+        oracle.set_threads(saved)

@@ -160,6 +160,14 @@ def test_deserialize_rejects(zkp, oracle, pyref):
     while pow((x ** 3 + 4) % P, (P - 1) // 2, P) == 1:
         x += 1
     b = bytearray(good); b[:48] = x.to_bytes(48, "big"); b[0] |= 0x80; cases.append(b)
+    # infinity flag with a non-zero x (G1 a, and G2 b in either half): the
+    # zcash encoding has one identity; anything else would be malleable
+    b = bytearray(good); b[0:48] = b"\xc0" + b"\0" * 47; b[17] = 1; cases.append(b)
+    b = bytearray(good); b[0] = 0xC1; b[1:48] = b"\0" * 47; cases.append(b)
+    b = bytearray(good); b[48:144] = b"\xc0" + b"\0" * 95; b[48 + 70] = 2; cases.append(b)
     for c in cases:
         with pytest.raises(ValueError):
             zkp.Proof.deserialize_compressed(bytes(c))
+    # the canonical identity encoding still decodes
+    b = bytearray(good); b[0:48] = b"\xc0" + b"\0" * 47
+    assert zkp.Proof.deserialize_compressed(bytes(b)).a[12] == 1

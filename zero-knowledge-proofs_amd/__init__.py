@@ -29,7 +29,7 @@ LIB_PATH = os.environ.get("ZK_AMD_LIB") or os.path.join(_HERE, "libzkp_amd.so")
 R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001  # Fr modulus
 
 ZK_OK, ZK_ERR_MSM_LEN, ZK_ERR_INVALID_WITNESS, ZK_ERR_QAP_DIVISION, ZK_ERR_DOMAIN, \
-    ZK_ERR_SETUP_PARAMS, ZK_ERR_DEVICE, ZK_ERR_RCCL, ZK_ERR_ARG = range(9)
+    ZK_ERR_SETUP_PARAMS, ZK_ERR_DEVICE, ZK_ERR_RCCL, ZK_ERR_ARG, ZK_ERR_DIMENSION = range(10)
 G1_WORDS, G2_WORDS = 13, 25
 PARTIAL_BYTES = 1536
 
@@ -45,8 +45,10 @@ EXPORTS = (
     "zk_proof_serialize_compressed", "zk_rccl_unique_id", "zk_ctx_attach_rccl",
     "zk_test_prove_virtual_shards", "zk_proof_deserialize_compressed", "zk_groth16_verify",
     "zk_groth16_verify_batch", "zk_pairing_product_is_one", "zk_msm_g1_upload_windows",
-    "zk_msm_g2_upload_windows",
+    "zk_msm_g2_upload_windows", "zk_build_id", "zk_ctx_set_schedule", "zk_qap_evaluate_at",
+    "zk_poly_evaluate_batch", "zk_synthetic_witness_dev",
 )
+CSRC = os.path.join(_HERE, "csrc")
 
 
 # ------------------------------------------------------------- errors ----
@@ -74,6 +76,10 @@ class DomainTooSmall(QAPError):
     pass
 
 
+class DimensionMismatch(QAPError):
+    """QAPError::FieldError(FieldError::DimensionMismatch), qap:191-198"""
+
+
 class SetupError(GrothError):
     """crates/groth16-setup/src/lib.rs:95-113 (InvalidParams)"""
 
@@ -85,7 +91,7 @@ class DeviceError(GrothError):
 _STATUS = {ZK_ERR_MSM_LEN: MSMError, ZK_ERR_INVALID_WITNESS: InvalidWitness,
            ZK_ERR_QAP_DIVISION: PolynomialDivisionFailed, ZK_ERR_DOMAIN: DomainTooSmall,
            ZK_ERR_SETUP_PARAMS: SetupError, ZK_ERR_DEVICE: DeviceError,
-           ZK_ERR_RCCL: DeviceError, ZK_ERR_ARG: ValueError}
+           ZK_ERR_RCCL: DeviceError, ZK_ERR_ARG: ValueError, ZK_ERR_DIMENSION: DimensionMismatch}
 
 
 # ---------------------------------------------------------- C structs ----
@@ -153,10 +159,11 @@ def lib():
         L.zk_ctx_destroy.argtypes = [C.c_void_p]
         L.zk_last_error.restype = C.c_char_p
         L.zk_last_error.argtypes = [C.c_void_p]
+        L.zk_build_id.restype = C.c_char_p
         for name in EXPORTS:
             f = getattr(L, name)
             if name not in ("zk_ctx_create", "zk_ctx_destroy", "zk_last_error",
-                            "zk_msm_bases_free", "zk_pk_free"):
+                            "zk_msm_bases_free", "zk_pk_free", "zk_build_id"):
                 f.restype = C.c_int
         L.zk_msm_bases_free.argtypes = [C.c_void_p]
         L.zk_pk_free.argtypes = [C.c_void_p]
@@ -166,6 +173,34 @@ def lib():
 
 def _p(a):
     return C.c_void_p(a.ctypes.data)
+
+
+def build_id():
+    """zk_build_id(): '<git HEAD>[-dirty] src:<source hash>' of the loaded library."""
+    return lib().zk_build_id().decode()
+
+
+def source_hash():
+    """sha256 (16 hex) over csrc/*.hip and *.hpp (sorted) + include/zkp.h of THIS
+    tree -- what the Makefile embeds in zk_build_id()."""
+    import hashlib
+    names = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".hpp")))
+    h = hashlib.sha256()
+    for f in names:
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    with open(os.path.join(os.path.dirname(_HERE), "include", "zkp.h"), "rb") as fh:
+        h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def check_build():
+    """Raise unless the loaded libzkp_amd.so was built from this tree's sources."""
+    bid = build_id()
+    want = source_hash()
+    if not bid.endswith("src:" + want):
+        raise ImportError(f"libzkp_amd.so build id {bid!r} does not match the sources (src:{want}); rebuild it")
+    return bid
 
 
 def _check(rc, ctx=None, what=""):
@@ -239,6 +274,20 @@ class Context:
         buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
         _check(lib().zk_ctx_attach_rccl(C.c_void_p(self._h), buf, C.c_int(rank), C.c_int(world)), self,
                "zk_ctx_attach_rccl")
+
+    def set_schedule(self, schedule=-1):
+        """zk_ctx_set_schedule: -1 default, 0 overlapped streams, 3 every prove
+        kernel in order on one stream (isolated kernel durations)."""
+        _check(lib().zk_ctx_set_schedule(C.c_void_p(self._h), C.c_int(int(schedule))), self, "zk_ctx_set_schedule")
+
+    def synthetic_witness(self, n, seed):
+        """The groth16-cli circuit's witness z (3n+1 canonical Fr) generated
+        on this GPU -> torch int64 tensor (3n+1, 4) on its device."""
+        import torch
+        z = torch.empty((3 * n + 1, 4), dtype=torch.int64, device=f"cuda:{self.device}")
+        _check(lib().zk_synthetic_witness_dev(C.c_void_p(self._h), C.c_uint64(n), C.c_uint64(seed),
+                                              C.c_void_p(z.data_ptr())), self, "zk_synthetic_witness_dev")
+        return z
 
     # ---- live kernel timing (HIP events on the launching stream) ----
     def profile(self, enable=True):
@@ -433,6 +482,59 @@ class QAP:
         """max(per-variable degree < n, deg Z = n) = n (qap:285-294)."""
         return self.domain_size
 
+    def evaluate_at(self, point, assignment, ctx=None):
+        """QAP::evaluate_at (qap:190-220) on the GPU -> QAPEvaluation with
+        A(point), B(point), C(point) = sum_i z_i A_i(point) ..., Z(point)."""
+        ctx = ctx or default_context()
+        z = _fr_rows(assignment)
+        out = (_Fr * 4)()
+        rc = lib().zk_qap_evaluate_at(C.c_void_p(ctx._h), C.byref(self.csr.s), C.byref(_fr(point)),
+                                      _p(z) if len(z) else None, C.c_size_t(len(z)), out)
+        _check(rc, ctx, "zk_qap_evaluate_at")
+        a, b, c, zv = (from_limbs(list(o.l)) for o in out)
+        return QAPEvaluation(a, b, c, zv)
+
+    @staticmethod
+    def verify_evaluation(ev):
+        """QAP::verify_evaluation (qap:274-282)."""
+        if ev.h_val is not None:
+            return (ev.a_val * ev.b_val - ev.c_val) % R == ev.h_val * ev.z_val % R
+        return ev.a_val * ev.b_val % R == ev.c_val
+
+
+class QAPEvaluation:
+    """QAPEvaluation (crates/groth16-qap/src/lib.rs:49-57): field values as ints."""
+
+    def __init__(self, a_val, b_val, c_val, z_val, h_val=None):
+        self.a_val, self.b_val, self.c_val, self.z_val, self.h_val = a_val, b_val, c_val, z_val, h_val
+
+
+def batch_evaluate(polynomials, point, ctx=None):
+    """qap utils::batch_evaluate (qap:315-322) on the GPU: each polynomial is
+    a coefficient list (lowest degree first) of Fr ints or an (m, 4) array."""
+    ctx = ctx or default_context()
+    rows = [_fr_rows(p) if len(p) else np.zeros((0, 4), dtype=np.uint64) for p in polynomials]
+    offs = np.zeros(len(rows) + 1, dtype=np.uint64)
+    for i, r in enumerate(rows):
+        offs[i + 1] = offs[i] + len(r)
+    flat = np.ascontiguousarray(np.concatenate(rows) if rows else np.zeros((0, 4), dtype=np.uint64))
+    out = np.zeros((max(len(rows), 1), 4), dtype=np.uint64)
+    rc = lib().zk_poly_evaluate_batch(C.c_void_p(ctx._h), _p(flat) if len(flat) else None, _p(offs),
+                                      C.c_size_t(len(rows)), C.byref(_fr(point)), _p(out))
+    _check(rc, ctx, "zk_poly_evaluate_batch")
+    return [from_limbs(o) for o in out[:len(rows)]]
+
+
+_default_ctx = None
+
+
+def default_context():
+    """Context(0), created on first use (for reference-shaped calls that take no ctx)."""
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
 
 # -------------------------------------------------------------- setup ----
 class SetupParams:
@@ -591,6 +693,8 @@ class Witness:
         if not isinstance(a, np.ndarray):
             a = fr_array(a)
         a = np.ascontiguousarray(a, dtype=np.uint64).reshape(-1, 4)
+        if not fr_rows_canonical(a):
+            raise ValueError("assignment holds a value >= r (not a canonical Fr)")
         if num_public >= len(a):
             raise InvalidWitness("Number of public inputs must be less than total assignment length")
         if len(a) == 0 or not (a[0, 0] == 1 and not a[0, 1:].any()):
@@ -599,7 +703,26 @@ class Witness:
         self.num_public = num_public
 
     def public_inputs(self):
+        """core:101-104"""
         return self.assignment[1:self.num_public + 1]
+
+    def private_inputs(self):
+        """core:106-109"""
+        return self.assignment[self.num_public + 1:]
+
+
+_R_LIMBS = np.array([(R >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)], dtype=np.uint64)
+
+
+def fr_rows_canonical(a):
+    """Every row (4 little-endian u64 limbs) < r, vectorised."""
+    a = np.asarray(a, dtype=np.uint64).reshape(-1, 4)
+    lt = np.zeros(len(a), dtype=bool)
+    eq = np.ones(len(a), dtype=bool)
+    for i in (3, 2, 1, 0):
+        lt |= eq & (a[:, i] < _R_LIMBS[i])
+        eq &= a[:, i] == _R_LIMBS[i]
+    return bool(lt.all())
 
 
 class Proof:

@@ -119,12 +119,56 @@ int zk_ctx_synchronize(zk_ctx* ctx) {
 }
 
 // ------------------------------------------------------------------ MSM ---
+// Scalars must be canonical Fr (< r, as ark's Fr always is) of at most
+// scalar_bits bits; anything else is ZK_ERR_ARG rather than a silently
+// different sum.
+static bool scalar_ok(const zk_fr& a, uint32_t bits) {
+  if (!fr_canonical(a)) return false;
+  for (uint32_t w = 0; w < 4; w++) {
+    const uint32_t lo = 64 * w;
+    if (bits >= lo + 64) continue;
+    const uint64_t allowed = bits <= lo ? 0 : (~0ull >> (64 - (bits - lo)));
+    if (a.l[w] & ~allowed) return false;
+  }
+  return true;
+}
+// flags |= 1 when a device scalar is >= r or wider than bits
+__global__ void __launch_bounds__(256) k_check_scalars(const uint64_t* __restrict__ sc, size_t n, uint32_t bits,
+                                                       uint32_t* __restrict__ flags) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t l[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) l[w] = sc[4 * i + w];
+  const uint64_t R[4] = {0xffffffff00000001ull, 0x53bda402fffe5bfeull, 0x3339d80809a1d805ull,
+                        0x73eda753299d7d48ull};
+  bool lt = false, decided = false;
+#pragma unroll
+  for (int w = 3; w >= 0; w--) {
+    if (!decided && l[w] != R[w]) { lt = l[w] < R[w]; decided = true; }
+  }
+  bool ok = lt;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    const uint32_t lo = 64 * w;
+    if (bits >= lo + 64) continue;
+    const uint64_t allowed = bits <= lo ? 0 : (~0ull >> (64 - (bits - lo)));
+    ok = ok && !(l[w] & ~allowed);
+  }
+  if (!ok) atomicOr(flags, 1u);
+}
+
 template <class C, class ABI>
 static int msm_host(zk_ctx* ctx, const ABI* bases, size_t nb, const zk_fr* sc, size_t ns, uint32_t bits,
                     ABI* out) {
   if (!ctx || !out) return ZK_ERR_ARG;
   if (nb != ns) return ZK_ERR_MSM_LEN;  // ark VariableBaseMSM::msm -> Err(min_len)
   if (bits == 0 || bits > 256 || nb > 0x7fffffffull) return ZK_ERR_ARG;
+  for (size_t i = 0; i < ns; i++)
+    if (!scalar_ok(sc[i], bits)) {
+      ctx->err = "scalar " + std::to_string(i) + " is not a canonical Fr of at most scalar_bits bits";
+      return ZK_ERR_ARG;
+    }
   ZK_GUARD(ctx, {
     hipStream_t st = ctx->stream;
     const int sw = bits <= 64 ? 1 : 4;
@@ -231,6 +275,14 @@ static int msm_dev(zk_ctx* ctx, const zk_msm_bases* b, const void* d_sc, size_t 
   ZK_GUARD(ctx, {
     hipStream_t st = ctx->stream;
     const uint64_t* sc = reinterpret_cast<const uint64_t*>(d_sc);
+    ctx->flags.ensure(16);
+    ctx->flags_host.ensure(16);
+    ZK_HIP(hipMemsetAsync(ctx->flags.p, 0, 4, st));
+    if (n) {
+      k_check_scalars<<<ceil_div(n, 256), 256, 0, st>>>(sc, n, bits, ctx->flags.as<uint32_t>());
+      ZK_LAUNCH_CHECK();
+    }
+    ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
     int sw = 4;
     if (bits <= 64) {
       ctx->tmp_scal.ensure(sizeof(uint64_t) * std::max<size_t>(n, 1));
@@ -250,6 +302,10 @@ static int msm_dev(zk_ctx* ctx, const zk_msm_bases* b, const void* d_sc, size_t 
     msm_download<C>(w, st);
     ZK_HIP(hipStreamSynchronize(st));
     ctx->prof.collect();
+    if (*ctx->flags_host.as<uint32_t>()) {
+      ctx->err = "a device scalar is not a canonical Fr of at most scalar_bits bits";
+      return ZK_ERR_ARG;
+    }
     host_to_abi<C>(msm_finish<C>(w), reinterpret_cast<uint64_t*>(out));
     return ZK_OK;
   })

@@ -42,6 +42,7 @@ struct zk_ctx {
   zk::Prof prof;
   std::unique_ptr<zk::Exchange> exch;          // RCCL communicator (sharded prover), if attached
   zk::DistQ dq;                                // distributed-quotient buffers
+  int sched = -1;                              // zk_ctx_set_schedule (-1: ZK_PROVE_SCHED / default)
 
   zk::NttDomain& domain(uint32_t log_n);
 };
@@ -67,6 +68,10 @@ namespace zk {
 // Expand every slot's bases into the window-shifted copies the shared-bucket
 // MSM reads (ZK_MSM_PRECOMP=0 keeps one copy and per-window buckets).
 void pk_precompute_windows(zk_ctx* ctx, zk_pk_dev& pk);
+// canonical-input checks (prove.hip): a < r on the host; on the device,
+// flags |= 8 when some of the n canonical Fr at d_z is >= r
+bool fr_canonical(const zk_fr& a);
+void check_canonical(const void* d_z, uint64_t n, uint32_t* d_flags, hipStream_t st);
 }
 
 struct zk_msm_bases {

@@ -284,8 +284,20 @@ void dist_quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, Exchan
 
 struct RcclExchange : Exchange {
   ncclComm_t comm = nullptr;
+  DevBuf stat;
+  PinnedBuf stat_host;
   void all_to_all(const void* send, void* recv, size_t chunk_bytes, hipStream_t st) override {
     ZK_NCCL(ncclAllToAll(send, recv, chunk_bytes, ncclUint8, comm, st));
+  }
+  int agree_max(int status, hipStream_t st) override {
+    stat.ensure(16);
+    stat_host.ensure(16);
+    *stat_host.as<int32_t>() = status;
+    ZK_HIP(hipMemcpyAsync(stat.p, stat_host.p, 4, hipMemcpyHostToDevice, st));
+    ZK_NCCL(ncclAllReduce(stat.p, stat.p, 1, ncclInt32, ncclMax, comm, st));
+    ZK_HIP(hipMemcpyAsync(stat_host.p, stat.p, 4, hipMemcpyDeviceToHost, st));
+    ZK_HIP(hipStreamSynchronize(st));
+    return *stat_host.as<int32_t>();
   }
   ~RcclExchange() override {
     if (comm) (void)ncclCommDestroy(comm);

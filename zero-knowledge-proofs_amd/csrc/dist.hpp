@@ -28,6 +28,8 @@ namespace zk {
 struct Exchange {
   int rank = 0, world = 1;
   virtual void all_to_all(const void* send, void* recv, size_t chunk_bytes, hipStream_t st) = 0;
+  // max over ranks of a host status code (synchronous)
+  virtual int agree_max(int status, hipStream_t st) = 0;
   virtual ~Exchange() = default;
 };
 

@@ -129,6 +129,34 @@ __global__ void k_set_extras(uint64_t* __restrict__ dst, Extras e, uint32_t n) {
   if (threadIdx.x < n) dst[threadIdx.x] = e.v[threadIdx.x];
 }
 
+// flags bit 3: some z_i >= r.  The reference's assignment is a vector of
+// reduced Fr (core:40-44), so a non-canonical limb vector has no reference
+// meaning (its lo64 would differ from the reduced value's): ZK_ERR_ARG.
+__global__ void __launch_bounds__(256) k_check_canonical(const Fr* __restrict__ z, uint64_t n,
+                                                         uint32_t* __restrict__ flags) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Fr a = ld_vec(&z[i]);
+  uint32_t br = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) (void)__builtin_subc(a.v[k], FrParams::MOD[k], br, &br);
+  if (!br) atomicOr(flags, 8u);   // a - r did not borrow: a >= r
+}
+
+void check_canonical(const void* d_z, uint64_t n, uint32_t* d_flags, hipStream_t st) {
+  if (!n) return;
+  k_check_canonical<<<ceil_div(n, 256), 256, 0, st>>>(reinterpret_cast<const Fr*>(d_z), n, d_flags);
+  ZK_LAUNCH_CHECK();
+}
+
+bool fr_canonical(const zk_fr& a) {
+  static const uint64_t R[4] = {0xffffffff00000001ull, 0x53bda402fffe5bfeull, 0x3339d80809a1d805ull,
+                                0x73eda753299d7d48ull};
+  for (int i = 3; i >= 0; i--)
+    if (a.l[i] != R[i]) return a.l[i] < R[i];
+  return false;
+}
+
 // ------------------------------------------------------------- pk upload ---
 static uint64_t shard_lo(uint64_t len, uint32_t k, uint32_t ns) { return len * k / ns; }
 
@@ -359,6 +387,14 @@ static bool dist_quotient_enabled() {
   return !(e && std::strcmp(e, "0") == 0);
 }
 
+// A sharded key whose ctx is attached to the matching RCCL communicator
+// computes its quotient distributed (three all-to-alls per proof).
+static bool uses_dist_quotient(const zk_ctx* ctx, const zk_pk_dev* pk) {
+  return pk->nshards > 1 && ctx->exch && ctx->exch->world == (int)pk->nshards &&
+         ctx->exch->rank == (int)pk->shard && dist_quotient_ok(pk->n, (int)pk->nshards) &&
+         dist_quotient_enabled();
+}
+
 // h_given (virtual-rank tests): this shard's lo64(H_(shard + nshards d)) is
 // already on the device, with the witness-check flags of all ranks.
 static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, const zk_fr* r,
@@ -370,6 +406,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   ctx->flags.ensure(16);
   const int ph_span = ctx->prof.begin(st, "prove_gpu_span", pk->n);   // first kernel .. last MSM done
   ZK_HIP(hipMemsetAsync(ctx->flags.p, 0, 16, st));
+  check_canonical(d_z, pk->V, ctx->flags.as<uint32_t>(), st);   // every z_i < r, else ZK_ERR_ARG
   // The five MSMs are independent.  Streams (<= GPU_MAX_HW_QUEUES = 4, so no
   // two share a hardware queue): main (high priority) runs the quotient and
   // then the H MSM that depends on it; side[0] (high priority) the G2 MSM,
@@ -377,10 +414,11 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   // Latency-bound phases (scan, bucket reduction) of one MSM overlap the
   // throughput-bound accumulation of another.
   ZK_HIP(hipEventRecord(ctx->ev_scal, st));           // z (and flags reset) ready
-  static const int sched = [] {
+  static const int sched_env = [] {
     const char* e = getenv("ZK_PROVE_SCHED");
     return e ? atoi(e) : 0;
   }();
+  const int sched = ctx->sched >= 0 ? ctx->sched : sched_env;   // zk_ctx_set_schedule overrides
   auto stream_of = [&](int slot) {
     if (sched == 3) return st;   // fully serial (per-phase profiling)
     return slot == MSM_H ? st : slot == MSM_B2 ? ctx->side[0] : slot == MSM_IC ? ctx->side[1] : ctx->side[2];
@@ -388,9 +426,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   // The quotient: local (every coefficient), distributed over the RCCL
   // ranks of a sharded key (this rank's coefficients i = shard mod N), or
   // given (virtual-rank tests).
-  const bool dist = !h_given && pk->nshards > 1 && ctx->exch && ctx->exch->world == (int)pk->nshards &&
-                    ctx->exch->rank == (int)pk->shard && dist_quotient_ok(pk->n, (int)pk->nshards) &&
-                    dist_quotient_enabled();
+  const bool dist = !h_given && uses_dist_quotient(ctx, pk);
   const uint64_t* h_src = h_given ? h_given : ctx->tmp_scal.as<uint64_t>();
   const uint32_t h_div = (h_given || dist) ? pk->nshards : 1;
   auto run_quotient = [&]() {
@@ -610,14 +646,18 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   ctx->prof.collect();
   const uint32_t flags = h_given ? given_flags : *ctx->flags_host.as<uint32_t>();
   p.status = ZK_OK;
-  if (flags & 5u) p.status = ZK_ERR_INVALID_WITNESS;
+  if (flags & 8u) p.status = ZK_ERR_ARG;
+  else if (flags & 5u) p.status = ZK_ERR_INVALID_WITNESS;
   else if (flags & 2u) p.status = ZK_ERR_QAP_DIVISION;
   return p;
 }
 
 static int combine(const Partial* parts, size_t k, zk_proof* out) {
-  // the witness checks are spread over the ranks' rows: InvalidWitness
-  // (core:83-98, 124-128) wins over the division failure (qap:266)
+  // the witness checks are spread over the ranks' rows: a non-canonical
+  // input (ZK_ERR_ARG) first, then InvalidWitness (core:83-98, 124-128)
+  // wins over the division failure (qap:266)
+  for (size_t i = 0; i < k; i++)
+    if (parts[i].status == ZK_ERR_ARG) return ZK_ERR_ARG;
   for (size_t i = 0; i < k; i++)
     if (parts[i].status == ZK_ERR_INVALID_WITNESS) return ZK_ERR_INVALID_WITNESS;
   for (size_t i = 0; i < k; i++)
@@ -639,6 +679,7 @@ static int combine(const Partial* parts, size_t k, zk_proof* out) {
 int prove_impl(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, size_t zlen, size_t num_public,
                const zk_fr* r, const zk_fr* s, zk_proof* out) {
   // Witness::new (core:81-99) and the length check of validate (core:113-118)
+  if (!fr_canonical(*r) || !fr_canonical(*s)) return ZK_ERR_ARG;   // Fr::rand draws are reduced
   if (num_public >= zlen) return ZK_ERR_INVALID_WITNESS;
   if (zlen != pk->V) return ZK_ERR_INVALID_WITNESS;
   if (pk->nshards != 1) return ZK_ERR_ARG;
@@ -650,8 +691,18 @@ int prove_partial_impl(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, size_t
                        const zk_fr* r, const zk_fr* s, zk_prove_partial* out) {
   std::memset(out, 0, sizeof *out);
   Partial p{};
-  if (num_public >= zlen || zlen != pk->V) {
-    p.status = ZK_ERR_INVALID_WITNESS;
+  int local = ZK_OK;
+  if (!fr_canonical(*r) || !fr_canonical(*s)) local = ZK_ERR_ARG;
+  else if (num_public >= zlen || zlen != pk->V) local = ZK_ERR_INVALID_WITNESS;
+  // Ranks of a distributed quotient agree on the host-side checks before
+  // the first all-to-all: a rank that bailed out alone would leave its
+  // peers blocked in the collective.
+  if (uses_dist_quotient(ctx, pk)) {
+    const int agreed = ctx->exch->agree_max(local, ctx->stream);
+    if (local == ZK_OK) local = agreed;
+  }
+  if (local != ZK_OK) {
+    p.status = local;
   } else {
     p = prove_partial(ctx, pk, reinterpret_cast<const uint64_t*>(d_z), r, s);
   }
@@ -669,6 +720,7 @@ int prove_virtual_shards_impl(zk_ctx* ctx, const zk_pk_dev* const* pks, uint32_t
   for (uint32_t k = 0; k < N; k++)
     if (!pks[k] || pks[k]->shard != k || pks[k]->nshards != N || pks[k]->n != pks[0]->n) return ZK_ERR_ARG;
   const zk_pk_dev* pk0 = pks[0];
+  if (!fr_canonical(*r) || !fr_canonical(*s)) return ZK_ERR_ARG;
   if (num_public >= zlen || zlen != pk0->V) return ZK_ERR_INVALID_WITNESS;
   if (!dist_quotient_ok(pk0->n, (int)N)) return ZK_ERR_ARG;
   hipStream_t st = ctx->stream;
@@ -679,6 +731,7 @@ int prove_virtual_shards_impl(zk_ctx* ctx, const zk_pk_dev* const* pks, uint32_t
   DevBuf flags;
   flags.ensure(sizeof(uint32_t) * N);
   ZK_HIP(hipMemsetAsync(flags.p, 0, sizeof(uint32_t) * N, st));
+  check_canonical(d_z, zlen, flags.as<uint32_t>(), st);
   auto exchange = [&](int which) {
     const size_t chunk = dq_chunk_bytes(pk0, (int)N, which);
     for (uint32_t a = 0; a < N; a++)
@@ -704,6 +757,7 @@ int prove_virtual_shards_impl(zk_ctx* ctx, const zk_pk_dev* const* pks, uint32_t
   ZK_HIP(hipStreamSynchronize(st));
   uint32_t all = 0;
   for (uint32_t f : hf) all |= f;
+  if (all & 8u) return ZK_ERR_ARG;
   std::vector<Partial> parts(N);
   for (uint32_t k = 0; k < N; k++) parts[k] = prove_partial(ctx, pks[k], z, r, s, hb[k].as<uint64_t>(), all);
   return combine(parts.data(), N, out);

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "ctx.hpp"
+#include "quotient.hpp"
 
 namespace zk {
 
@@ -542,6 +543,93 @@ int setup_impl(zk_ctx* ctx, const zk_r1cs_csr* q, const zk_setup_params* P, uint
   build_slot(MSM_H, false, hh, sh, n, 0, none, 0, /*strided*/ true);
   pk_precompute_windows(ctx, *d);
   *pk_dev = d.release();
+  return ZK_OK;
+}
+
+// ---------------------------------------------------- QAP::evaluate_at ---
+// A(t) = sum_i z_i A_i(t) = sum_j (Az)_j L_j(t) (A_i interpolates column i of
+// the constraint matrix over the domain, qap:143-170; columns >= V dropped,
+// qap:122-124), likewise B, C; Z(t) = t^n - 1 (qap:173-176, 211).
+__global__ void __launch_bounds__(256) k_eval_rows(CsrArgs m, const Fr* __restrict__ zc, uint64_t nc, uint64_t V,
+                                                   const Fr* __restrict__ L, Fr* __restrict__ out) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nc) return;
+  const Fr l = ld_vec(&L[j]);
+#pragma unroll
+  for (int k = 0; k < 3; k++) st_vec(&out[k * nc + j], fp_mul(row_dot(m.rp[k], m.col[k], m.val[k], j, zc, V), l));
+}
+// out[b] = sum of in[i] over i = b, b + stride, ... (per block b: one LDS tree)
+__global__ void __launch_bounds__(256) k_fr_sum(const Fr* __restrict__ in, uint64_t n, Fr* __restrict__ out) {
+  __shared__ Fr part[256];
+  Fr acc = fp_zero<FrParams>();
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    acc = fp_add(acc, ld_vec(&in[i]));
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  for (unsigned h = 128; h > 0; h >>= 1) {
+    if (threadIdx.x < h) part[threadIdx.x] = fp_add(part[threadIdx.x], part[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) st_vec(&out[blockIdx.x], part[0]);
+}
+
+// sum of n device Fr (Montgomery) -> host canonical
+static void fr_sum_to_host(const Fr* d_in, uint64_t n, zk_fr* out, hipStream_t st) {
+  DevBuf part;
+  const uint32_t nb = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(ceil_div(n, 256), 1), 1024);
+  part.ensure(sizeof(Fr) * (nb + 1));
+  k_fr_sum<<<nb, 256, 0, st>>>(d_in, n, part.as<Fr>());
+  ZK_LAUNCH_CHECK();
+  k_fr_sum<<<1, 256, 0, st>>>(part.as<Fr>(), nb, part.as<Fr>() + nb);
+  ZK_LAUNCH_CHECK();
+  fr_from_mont(part.as<Fr>() + nb, reinterpret_cast<uint64_t*>(part.as<Fr>() + nb), 1, st);
+  ZK_HIP(hipMemcpyAsync(out, part.as<Fr>() + nb, sizeof(zk_fr), hipMemcpyDeviceToHost, st));
+  ZK_HIP(hipStreamSynchronize(st));
+}
+
+int qap_evaluate_impl(zk_ctx* ctx, const zk_r1cs_csr* q, const zk_fr* point, const zk_fr* z, size_t zlen,
+                      zk_fr out[4]) {
+  hipStream_t st = ctx->stream;
+  const uint64_t V = q->num_variables, nc = q->num_constraints;
+  if (zlen != V) return ZK_ERR_DIMENSION;   // qap:191-198
+  if (!fr_canonical(*point)) return ZK_ERR_ARG;
+  for (size_t i = 0; i < zlen; i++)
+    if (!fr_canonical(z[i])) return ZK_ERR_ARG;
+  uint64_t n = 1;
+  while (n < nc) n <<= 1;
+  const uint32_t log_n = (uint32_t)__builtin_ctzll(n);
+  if (log_n > 32) return ZK_ERR_DOMAIN;
+  auto to_dev = [](const host::Fr& h) { Fr d; const host::Fr v = host::fr_to_dev(h); std::memcpy(d.v, v.l, 32); return d; };
+  const host::Fr t = host::fr_to_mont(point->l);
+  host::Fr tn = t;
+  for (uint32_t i = 0; i < log_n; i++) tn = host::fr_mul(tn, tn);
+  const host::Fr zt = host::fr_sub(tn, host::fr_one());
+  host::fr_from_mont(zt, out[3].l);
+  for (int k = 0; k < 3; k++) std::memset(out[k].l, 0, 32);
+  if (nc == 0) return ZK_OK;
+  DevBuf wpow, L, dz, rows;
+  CsrDev csr;
+  csr_upload(csr, q, st);
+  wpow.ensure(sizeof(Fr) * n);
+  L.ensure(sizeof(Fr) * n);
+  Fr one_d, w_d;
+  for (int i = 0; i < 8; i++) one_d.v[i] = FrParams::ONE[i];
+  for (int i = 0; i < 8; i++) w_d.v[i] = FR_ROOTS[log_n][i];
+  fr_powers(wpow.as<Fr>(), w_d, one_d, n, st);
+  if (host::fr_is_zero(zt)) {
+    k_lagrange_point<<<ceil_div(n, 256), 256, 0, st>>>(wpow.as<Fr>(), to_dev(t), n, L.as<Fr>());
+  } else {
+    const host::Fr kk = host::fr_mul(zt, host::fr_inv(host::fr_from_u64(n)));
+    k_lagrange<<<ceil_div(ceil_div(n, LAG_CHUNK), 256), 256, 0, st>>>(wpow.as<Fr>(), to_dev(t), to_dev(kk), n,
+                                                                      L.as<Fr>());
+  }
+  ZK_LAUNCH_CHECK();
+  dz.ensure(sizeof(zk_fr) * std::max<size_t>(zlen, 1));
+  if (zlen) ZK_HIP(hipMemcpyAsync(dz.p, z, sizeof(zk_fr) * zlen, hipMemcpyHostToDevice, st));
+  rows.ensure(sizeof(Fr) * 3 * nc);
+  k_eval_rows<<<ceil_div(nc, 256), 256, 0, st>>>(csr_args(csr), dz.as<Fr>(), nc, V, L.as<Fr>(), rows.as<Fr>());
+  ZK_LAUNCH_CHECK();
+  for (int k = 0; k < 3; k++) fr_sum_to_host(rows.as<Fr>() + k * nc, nc, &out[k], st);
   return ZK_OK;
 }
 

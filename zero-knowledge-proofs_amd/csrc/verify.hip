@@ -116,14 +116,21 @@ bool is_zero6(const uint64_t* c) {
 
 // zcash / ark-bls12-381 0.4 compressed point, validated like
 // CanonicalDeserialize::deserialize_compressed (Validate::Yes): compression
-// flag set, infinity without the sort flag, x < p, x^3 + b a square, the
-// flagged root, the prime-order subgroup.
+// flag set, infinity without the sort flag and with every x byte zero (the
+// zcash encoding has exactly one identity: anything else would make a
+// malleable proof encoding), x < p, x^3 + b a square, the flagged root, the
+// prime-order subgroup.
+static bool x_bytes_zero(const uint8_t* in, size_t len) {
+  uint8_t acc = in[0] & 0x1f;   // flag bits masked off
+  for (size_t i = 1; i < len; i++) acc |= in[i];
+  return acc == 0;
+}
 int decode_g1(const uint8_t* in, zk_g1_affine& out) {
   std::memset(&out, 0, sizeof out);
   const uint8_t f = in[0];
   if (!(f & 0x80)) return ZK_ERR_ARG;
   if (f & 0x40) {
-    if (f & 0x20) return ZK_ERR_ARG;
+    if ((f & 0x20) || !x_bytes_zero(in, 48)) return ZK_ERR_ARG;
     out.infinity = 1;
     return ZK_OK;
   }
@@ -147,7 +154,7 @@ int decode_g2(const uint8_t* in, zk_g2_affine& out) {
   const uint8_t f = in[0];
   if (!(f & 0x80)) return ZK_ERR_ARG;
   if (f & 0x40) {
-    if (f & 0x20) return ZK_ERR_ARG;
+    if ((f & 0x20) || !x_bytes_zero(in, 96)) return ZK_ERR_ARG;
     out.infinity = 1;
     return ZK_OK;
   }

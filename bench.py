@@ -115,8 +115,13 @@ def roofline_from(prof, log_n, overlapped=None):
     stream (zk_ctx_set_schedule 3), so a launch's HIP-event span is the
     kernel's own duration; `overlapped` (the timed region's four-stream
     schedule) is reported beside it."""
-    g1 = prof.get("msm_accum_g1", {"ms": 0.0, "launches": 0, "units": 0})
-    ms, launches, units = g1["ms"], g1["launches"], g1["units"]
+    def accum(pr):   # serial runs tag phases per MSM ("ABI/msm_accum_g1", "H/msm_accum_g1")
+        ms = launches = units = 0
+        for k, v in pr.items():
+            if k.split("/")[-1] == "msm_accum_g1":
+                ms, launches, units = ms + v["ms"], launches + v["launches"], units + v["units"]
+        return ms, launches, units
+    ms, launches, units = accum(prof)
     if ms <= 0 or launches == 0:
         return None
     algo_bytes = G1_PAIR_BYTES * units
@@ -133,9 +138,9 @@ def roofline_from(prof, log_n, overlapped=None):
                     "frac": round(tmads / VALU_PEAK_TMADS, 4)},
            "note": "integer-VALU bound (381-bit Montgomery products), not HBM; see DESIGN.md"}
     if overlapped:
-        o = overlapped.get("msm_accum_g1")
-        if o and o["launches"]:
-            out["overlapped_avg_launch_ms"] = round(o["ms"] / o["launches"], 4)
+        oms, ola, _ = accum(overlapped)
+        if ola:
+            out["overlapped_avg_launch_ms"] = round(oms / ola, 4)
     return out
 
 

@@ -10,7 +10,6 @@ import socket
 import subprocess
 import sys
 
-import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -49,4 +48,3 @@ def test_bench_two_rank_path_matches_single_gpu(ctx, zkp):
     proof = zkp.Prover.prove_device(dpk, z.data_ptr(), 3 * n + 1, 1, r, s)
     dpk.free()
     assert rec["proof_compressed"] == proof.serialize_compressed().hex()
-    del np

@@ -491,7 +491,7 @@ class QAP:
         rc = lib().zk_qap_evaluate_at(C.c_void_p(ctx._h), C.byref(self.csr.s), C.byref(_fr(point)),
                                       _p(z) if len(z) else None, C.c_size_t(len(z)), out)
         _check(rc, ctx, "zk_qap_evaluate_at")
-        a, b, c, zv = (from_limbs(list(o.l)) for o in out)
+        a, b, c, zv = (sum(int(x) << (64 * i) for i, x in enumerate(o.l)) for o in out)
         return QAPEvaluation(a, b, c, zv)
 
     @staticmethod

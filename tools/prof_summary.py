@@ -107,7 +107,92 @@ def stats(csv_path, out):
     print("\n".join(lines[:12]))
 
 
+def dispatches(db, counter):
+    """[(dispatch id, full kernel name, value KiB)] in dispatch order."""
+    cur = sqlite3.connect(db).cursor()
+    q = f"""select d.id, s.kernel_name, e.value from rocpd_pmc_event e
+            join rocpd_info_pmc p on e.pmc_id = p.id
+            join rocpd_kernel_dispatch d on d.event_id = e.event_id
+            join rocpd_info_kernel_symbol s on d.kernel_id = s.id
+            where p.name = '{counter}' order by d.id"""
+    return cur.execute(q).fetchall()
+
+
+def calib(fetch_db, write_db, out, log_path):
+    """FETCH_SIZE calibration of tools/gather_calib: counter bytes vs the
+    distinct 128-byte lines each kernel touches (printed by the program)."""
+    lines = {}
+    for ln in open(log_path):
+        m = re.match(r"(k_\w+(?:<[\d,]+>)?):\s+records (\d+) algorithmic_bytes (\d+) distinct_128B_lines (\d+)", ln)
+        if m:
+            lines[m.group(1)] = (int(m.group(2)), int(m.group(3)), int(m.group(4)))
+        m = re.match(r"k_stream: algorithmic_bytes (\d+)", ln)
+        if m:
+            lines["k_stream"] = (0, int(m.group(1)), int(m.group(1)) // 128)
+    names = {"_Z8k_gatherILi6ELi6E": "k_gather<6,6>", "_Z8k_gatherILi6ELi8E": "k_gather<6,8>",
+             "_Z8k_gatherILi8ELi8E": "k_gather<8,8>", "_Z8k_stream": "k_stream"}
+    f = {}
+    for _, k, v in dispatches(fetch_db, "FETCH_SIZE"):
+        for pre, nm in names.items():
+            if k.startswith(pre):
+                f.setdefault(nm, []).append(v * 1024)
+    w = {}
+    for _, k, v in dispatches(write_db, "WRITE_SIZE"):
+        for pre, nm in names.items():
+            if k.startswith(pre):
+                w.setdefault(nm, []).append(v * 1024)
+    res = {"note": "FETCH_SIZE (bytes) per dispatch vs the bytes of the distinct 128-B lines the kernel reads "
+                   "(+ its 4-byte index stream for the gathers); true_over_fetch = line bytes / FETCH_SIZE",
+           "kernels": {}}
+    for nm, (recs, algo, nl) in lines.items():
+        fv = sum(f.get(nm, [0])) / max(len(f.get(nm, [1])), 1)
+        line_bytes = nl * 128 + recs * 4
+        res["kernels"][nm] = {"records": recs, "algorithmic_bytes": algo, "line_bytes": line_bytes,
+                              "fetch_size_bytes": int(fv), "write_size_bytes": int(sum(w.get(nm, [0])) / max(len(w.get(nm, [1])), 1)),
+                              "true_over_fetch": round(line_bytes / fv, 3) if fv else None}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+def pmc_prove(fetch_db, write_db, out, factor):
+    """Per-dispatch FETCH/WRITE of a serial prove run; the accumulate
+    dispatches are split by their place in the prove (B2 G2, ABI batch, H)."""
+    fd, wd = dispatches(fetch_db, "FETCH_SIZE"), dispatches(write_db, "WRITE_SIZE")
+    agg = {}
+    for (_, k, fv), (_, k2, wv) in zip(fd, wd):
+        assert k == k2
+        a = agg.setdefault(short(k), [0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += fv * 1024
+        a[2] += wv * 1024
+    kernels = {k: {"dispatches": n, "fetch_bytes": int(fb / n), "write_bytes": int(wb / n),
+                   "traffic_guide_2x": int((2 * fb + wb) / n), "traffic_calibrated": int((factor * fb + wb) / n)}
+               for k, (n, fb, wb) in sorted(agg.items())}
+    acc = [(fv * 1024, wv * 1024) for (_, k, fv), (_, _, wv) in zip(fd, wd) if "k_msm_accum" in k and "pair" not in k]
+    res = {"note": f"serial prove (ZK_PROVE_SCHED=3); traffic_calibrated = {factor} x FETCH_SIZE + WRITE_SIZE "
+                   "(FETCH factor from tools/gather_calib for 96-byte gathers, profiles/r02_fetch_calibration.json); "
+                   "traffic_guide_2x = the guide's streaming correction",
+           "kernels": kernels}
+    if acc:
+        big = [a for a in acc if a[0] > 2e9]
+        small = [a for a in acc if a[0] <= 2e9]
+        per = lambda L: int(sum(factor * f + w for f, w in L) / len(L)) if L else None
+        res["msm_accum_g1_abi_bytes_per_launch"] = per(big)
+        res["msm_accum_g1_h_bytes_per_launch"] = per(small)
+        res["msm_accum_g1_bytes_per_launch"] = per(acc)
+    json.dump(res, open(out, "w"), indent=1)
+    for k, v in res.items():
+        if k != "kernels":
+            print(k, v)
+
+
 if __name__ == "__main__":
+    if sys.argv[1] == "calib":
+        calib(sys.argv[2], sys.argv[3], sys.argv[4], sys.argv[5])
+        sys.exit(0)
+    if sys.argv[1] == "pmc_prove":
+        pmc_prove(sys.argv[2], sys.argv[3], sys.argv[4], float(sys.argv[5]))
+        sys.exit(0)
     if sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3])
     elif sys.argv[1] == "trace":

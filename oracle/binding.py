@@ -188,6 +188,14 @@ def fft(data, inverse=False):
     return a
 
 
+def coset_fft(data, g, inverse=False):
+    a = np.ascontiguousarray(data, dtype=np.uint64).copy()
+    log_n = int(a.shape[0]).bit_length() - 1
+    lib().or_coset_fft(_p(a), C.c_uint32(log_n), C.c_int(int(inverse)),
+                       _p(np.array(int_to_limbs(g, 4), dtype=np.uint64)))
+    return a
+
+
 def quotient(csr, z, dense=False):
     n = domain_size(csr.num_constraints)
     h = np.zeros((n, 4), dtype=np.uint64)

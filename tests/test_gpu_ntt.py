@@ -23,6 +23,22 @@ def test_ntt_vs_oracle(ctx, oracle, log_n):
     assert np.array_equal(ctx.ntt(x, inverse=True), oracle.fft(x, inverse=True))
 
 
+@pytest.mark.parametrize("log_n", [0, 1, 4, 9, 10, 11, 15, 21])
+@pytest.mark.parametrize("g", [7, 5, 0x1234567890ABCDEF1234])
+def test_ntt_coset_vs_oracle(ctx, oracle, log_n, g):
+    """Radix2EvaluationDomain::coset_fft / coset_ifft with an arbitrary shift:
+    the first pass's fused g^i load factor and the bit reversal's n^-1 g^-i."""
+    x = oracle.random_fr(1 << log_n, 70 + log_n)
+    assert np.array_equal(ctx.ntt(x, coset=g), oracle.coset_fft(x, g))
+    assert np.array_equal(ctx.ntt(x, inverse=True, coset=g), oracle.coset_fft(x, g, inverse=True))
+
+
+def test_ntt_rejects_bad_coset(ctx, zkp, oracle):
+    x = oracle.random_fr(16, 3)
+    with pytest.raises(ValueError):
+        ctx.ntt(x, coset=0, inverse=True)
+
+
 def test_ntt_coset_roundtrip(ctx, oracle):
     x = oracle.random_fr(1 << 12, 99)
     y = ctx.ntt(x, coset=7)

@@ -1,0 +1,43 @@
+"""Run by tests/test_gpu_unfused.py in a child process with ZK_NTT_FUSE=0
+(read once per process): proves of the synthetic circuit at sizes whose
+quotient takes 1, 2 and 3+ NTT passes, through the UNFUSED quotient path
+(iNTT, separate coset scale, NTT), each checked against the C oracle."""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
+sys.path.insert(0, HERE)
+
+
+def main():
+    import importlib
+    import binding as oracle
+    import gpu_util as U
+    import pyref
+    zkp = importlib.import_module("zero-knowledge-proofs_amd")
+    assert os.environ.get("ZK_NTT_FUSE") == "0"
+    ctx = zkp.Context(0)
+    for log_n in [int(a) for a in sys.argv[1:]]:
+        n = 1 << log_n
+        rng = pyref.SplitMix64(900 + log_n)
+        params = [rng.fr() for _ in range(5)]
+        r, s = rng.fr(), rng.fr()
+        qap = zkp.QAP(zkp.CSRMatrices.synthetic(n))
+        crs = zkp.CRS.generate_from_qap(ctx, qap, zkp.SetupParams(*params), 1)
+        z = oracle.synthetic_witness(n, 901 + log_n)
+        rc, want = oracle.prove(U.oracle_pk_from(oracle, crs.pk), oracle.CSR.synthetic(n), z, 1, r, s)
+        assert rc == 0
+        got = zkp.Prover.prove(crs.pk.upload(ctx), zkp.Witness(z, 1), r=r, s=s)
+        if not np.array_equal(got.words, want):
+            print(f"MISMATCH at 2^{log_n}", flush=True)
+            sys.exit(1)
+        print(f"unfused 2^{log_n} ok", flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

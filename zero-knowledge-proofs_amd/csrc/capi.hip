@@ -320,37 +320,45 @@ int zk_msm_g2_dev(zk_ctx* ctx, const zk_msm_bases* b, const void* d_sc, size_t n
 }
 
 // ------------------------------------------------------------------ NTT ---
+// The transform runs on the canonical values as they are: with twiddles in
+// Montgomery form w R, a butterfly's fp_mul(v, w R) = v w, so canonical data
+// stay canonical through every pass and no to/from-Montgomery pass is needed.
+// Forward: DIF (its first pass reads d_data, scaled by g^i for a coset, into
+// the scratch) then the tiled bit reversal back into d_data; inverse: DIF
+// with the inverse twiddles, the bit reversal applying n^-1 (coset: n^-1 g^-i).
 static int ntt_device(zk_ctx* ctx, void* d_data, uint32_t log_n, int dir, const zk_fr* coset) {
   hipStream_t st = ctx->stream;
   const size_t n = (size_t)1 << log_n;
+  if (coset && !fr_canonical(*coset)) return ZK_ERR_ARG;
+  if (log_n == 0) return ZK_OK;   // a size-1 DFT (and its coset / inverse) is the identity
   NttDomain& dom = ctx->domain(log_n);
   ctx->tmp_fr.ensure(sizeof(Fr) * 2 * n);
   Fr* a = ctx->tmp_fr.as<Fr>();
   Fr* b = a + n;
-  auto to_dev = [](const host::Fr& h) { Fr d; const host::Fr v = host::fr_to_dev(h); std::memcpy(d.v, v.l, 32); return d; };
-  fr_to_mont(reinterpret_cast<const uint64_t*>(d_data), a, n, st);
+  Fr* d = reinterpret_cast<Fr*>(d_data);
+  auto to_dev = [](const host::Fr& h) { Fr x; const host::Fr v = host::fr_to_dev(h); std::memcpy(x.v, v.l, 32); return x; };
   const host::Fr one = host::fr_one();
   const host::Fr ninv = host::fr_inv(host::fr_from_u64(n));
   if (dir > 0) {
-    if (coset) {                                   // a_i *= g^i
+    const Fr* ltab = nullptr;
+    if (coset) {                                   // a_i *= g^i, fused into the first pass's load
       fr_powers(b, to_dev(host::fr_to_mont(coset->l)), to_dev(one), n, st);
-      fr_scale_table(a, b, log_n, false, st);
+      ltab = b;
     }
-    ntt_dif(a, dom, false, st, &ctx->prof);        // natural -> bit-reversed
-    fr_bitrev_copy(a, b, log_n, st);
+    ntt_dif(a, dom, false, st, &ctx->prof, d, ltab);   // natural d -> bit-reversed a
+    fr_bitrev_scale(a, d, log_n, nullptr, nullptr, st);
   } else {
-    ntt_dif(a, dom, true, st, &ctx->prof);
-    fr_bitrev_copy(a, b, log_n, st);
-    if (coset) {                                   // b_i *= n^-1 g^-i
+    ntt_dif(a, dom, true, st, &ctx->prof, d, nullptr);
+    if (coset) {                                   // out_i *= n^-1 g^-i
       host::Fr g = host::fr_to_mont(coset->l);
       if (host::fr_is_zero(g)) return ZK_ERR_ARG;
-      fr_powers(a, to_dev(host::fr_inv(g)), to_dev(ninv), n, st);
-      fr_scale_table(b, a, log_n, false, st);
+      fr_powers(b, to_dev(host::fr_inv(g)), to_dev(ninv), n, st);
+      fr_bitrev_scale(a, d, log_n, b, nullptr, st);
     } else {
-      fr_scale_const(b, to_dev(ninv), n, st);
+      const Fr c = to_dev(ninv);
+      fr_bitrev_scale(a, d, log_n, nullptr, &c, st);
     }
   }
-  fr_from_mont(b, reinterpret_cast<uint64_t*>(d_data), n, st);
   return ZK_OK;
 }
 

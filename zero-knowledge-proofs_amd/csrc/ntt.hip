@@ -20,29 +20,37 @@ constexpr int NTT_THREADS = (1 << NTT_TILE_LOG) >> NTT_R;
 // touches LDS once per round (16-byte accesses), so an 11-stage tile costs 4
 // LDS round trips and 4 barriers instead of 11.  Twiddle of local stage t
 // for row r: omega_(2^(t+1))^(r mod 2^t) = omega_2048^((r mod 2^t) 2^(10-t)).
-template <int R, int Q, bool DIT>
+template <int R, int Q, bool DIT, bool LSB0>
 __device__ __forceinline__ void ntt_stage(Fr (&x)[1 << R], const Fr* __restrict__ sm, uint32_t rlow, uint32_t lsb) {
   constexpr int G = 1 << R;
   const uint32_t t = lsb + Q;
+  // LSB0 (the round over local stages 0 .. R-1): rlow = 0, so twiddle k of
+  // stage Q is omega_2048^(k 2^(10-Q)) and k = 0 is 1 -- those butterflies
+  // skip their multiply (all of stage 0, half of stage 1, ...).
   Fr w[1 << Q];
 #pragma unroll
-  for (int k = 0; k < (1 << Q); k++) w[k] = ld_vec(&sm[(rlow + ((uint32_t)k << lsb)) << (NTT_SM_LOG - 1 - t)]);
+  for (int k = 0; k < (1 << Q); k++)
+    if (!(LSB0 && k == 0)) w[k] = ld_vec(&sm[(rlow + ((uint32_t)k << lsb)) << (NTT_SM_LOG - 1 - t)]);
 #pragma unroll
   for (int i = 0; i < G / 2; i++) {
     const int m = ((i >> Q) << (Q + 1)) | (i & ((1 << Q) - 1));
+    const int k = m & ((1 << Q) - 1);
     Fr u = x[m], v = x[m + (1 << Q)];
-    if (DIT) {
-      v = fp_mul(v, w[m & ((1 << Q) - 1)]);
+    if (LSB0 && k == 0) {
+      x[m] = fp_add(u, v);
+      x[m + (1 << Q)] = fp_sub(u, v);
+    } else if (DIT) {
+      v = fp_mul(v, w[k]);
       x[m] = fp_add(u, v);
       x[m + (1 << Q)] = fp_sub(u, v);
     } else {
       x[m] = fp_add(u, v);
-      x[m + (1 << Q)] = fp_mul(fp_sub(u, v), w[m & ((1 << Q) - 1)]);
+      x[m + (1 << Q)] = fp_mul(fp_sub(u, v), w[k]);
     }
   }
 }
 
-template <int R, bool DIT>
+template <int R, bool DIT, bool LSB0 = false>
 __device__ __forceinline__ void ntt_round(Fr* sh, const Fr* __restrict__ sm, uint32_t ns, uint32_t logC,
                                           uint32_t lsb) {
   constexpr int G = 1 << R;
@@ -56,16 +64,51 @@ __device__ __forceinline__ void ntt_round(Fr* sh, const Fr* __restrict__ sm, uin
 #pragma unroll
     for (int m = 0; m < G; m++) x[m] = ld_vec(&sh[((r0 + ((uint32_t)m << lsb)) << logC) | c]);
     if (DIT) {
-      ntt_stage<R, 0, DIT>(x, sm, rlow, lsb);
-      if constexpr (R > 1) ntt_stage<R, (R > 1 ? 1 : 0), DIT>(x, sm, rlow, lsb);
-      if constexpr (R > 2) ntt_stage<R, (R > 2 ? 2 : 0), DIT>(x, sm, rlow, lsb);
+      ntt_stage<R, 0, DIT, LSB0>(x, sm, rlow, lsb);
+      if constexpr (R > 1) ntt_stage<R, (R > 1 ? 1 : 0), DIT, LSB0>(x, sm, rlow, lsb);
+      if constexpr (R > 2) ntt_stage<R, (R > 2 ? 2 : 0), DIT, LSB0>(x, sm, rlow, lsb);
     } else {
-      if constexpr (R > 2) ntt_stage<R, (R > 2 ? 2 : 0), DIT>(x, sm, rlow, lsb);
-      if constexpr (R > 1) ntt_stage<R, (R > 1 ? 1 : 0), DIT>(x, sm, rlow, lsb);
-      ntt_stage<R, 0, DIT>(x, sm, rlow, lsb);
+      if constexpr (R > 2) ntt_stage<R, (R > 2 ? 2 : 0), DIT, LSB0>(x, sm, rlow, lsb);
+      if constexpr (R > 1) ntt_stage<R, (R > 1 ? 1 : 0), DIT, LSB0>(x, sm, rlow, lsb);
+      ntt_stage<R, 0, DIT, LSB0>(x, sm, rlow, lsb);
     }
 #pragma unroll
     for (int m = 0; m < G; m++) st_vec(&sh[((r0 + ((uint32_t)m << lsb)) << logC) | c], x[m]);
+  }
+}
+
+// The rounds of a tile's 2^ns-point sub-transform: DIF top-down (the last
+// round, over local stages 0 .., is the LSB0 one), DIT bottom-up (LSB0 first).
+template <bool DIT>
+__device__ __forceinline__ void ntt_rounds(Fr* sh, const Fr* __restrict__ sm, uint32_t ns, uint32_t logC) {
+  const uint32_t full = ns / NTT_R, rem = ns % NTT_R;
+  if (DIT) {
+    uint32_t lsb = 0;
+    if (rem == 1) {
+      ntt_round<1, true, true>(sh, sm, ns, logC, 0);
+      lsb = 1;
+      __syncthreads();
+    } else if (rem == 2) {
+      ntt_round<2, true, true>(sh, sm, ns, logC, 0);
+      lsb = 2;
+      __syncthreads();
+    }
+    for (uint32_t i = 0; i < full; i++, lsb += NTT_R) {
+      if (lsb == 0) ntt_round<NTT_R, true, true>(sh, sm, ns, logC, 0);
+      else ntt_round<NTT_R, true>(sh, sm, ns, logC, lsb);
+      __syncthreads();
+    }
+  } else {
+    uint32_t lsb = ns;
+    for (uint32_t i = 0; i < full; i++) {
+      lsb -= NTT_R;
+      if (lsb == 0) ntt_round<NTT_R, false, true>(sh, sm, ns, logC, 0);
+      else ntt_round<NTT_R, false>(sh, sm, ns, logC, lsb);
+      __syncthreads();
+    }
+    if (rem == 2) ntt_round<2, false, true>(sh, sm, ns, logC, 0);
+    if (rem == 1) ntt_round<1, false, true>(sh, sm, ns, logC, 0);
+    __syncthreads();
   }
 }
 
@@ -79,8 +122,9 @@ __device__ __forceinline__ void ntt_round(Fr* sh, const Fr* __restrict__ sm, uin
 // sum_a x[a n2 + b] w_n1^(a k1); sub-transforms in place leave element k at
 // bitrev(k1) n2 + bitrev(k2) = bitrev_(log n)(k): exactly radix-2 DIF order.
 template <bool DIT>
-__global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(Fr* __restrict__ data, NttTabs tabs, uint32_t log_n,
-                                                          uint32_t s_lo, uint32_t ns, uint32_t logC) {
+__global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(Fr* __restrict__ data, const Fr* src, const Fr* ltab,
+                                                          NttTabs tabs, uint32_t log_n, uint32_t s_lo, uint32_t ns,
+                                                          uint32_t logC) {
   extern __shared__ uint4 sh_raw[];
   Fr* sh = reinterpret_cast<Fr*>(sh_raw);
   const uint32_t C = 1u << logC;
@@ -92,34 +136,18 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(Fr* __restrict__ data,
   const size_t base = ((size_t)hi << (s_lo + ns)) + lo0;
   const uint32_t tw_shift = log_n - s_lo - ns;          // omega_N = omega_n^(2^tw_shift)
 
+  // src: the first pass of an out-of-place transform reads another buffer;
+  // ltab: an elementwise factor on load (a coset's g^i, natural order)
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) {
     const uint32_t r = k >> logC, c = k & (C - 1);
-    Fr v = ld_vec(&data[base + ((size_t)r << s_lo) + c]);
+    const size_t gi = base + ((size_t)r << s_lo) + c;
+    Fr v = ld_vec(&src[gi]);
+    if (ltab) v = fp_mul(v, ld_vec(&ltab[gi]));
     if (DIT && s_lo) v = fp_mul(v, tw_full(tabs, ((lo0 + c) * bitrev32(r, ns)) << tw_shift, log_n));
     st_vec(&sh[k], v);
   }
   __syncthreads();
-  // rounds of NTT_R stages (fewer for the remainder): DIF top-down, DIT bottom-up
-  const uint32_t full = ns / NTT_R, rem = ns % NTT_R;
-  if (DIT) {
-    uint32_t lsb = 0;
-    for (uint32_t i = 0; i < full; i++, lsb += NTT_R) {
-      ntt_round<NTT_R, true>(sh, tabs.sm, ns, logC, lsb);
-      __syncthreads();
-    }
-    if (rem == 2) ntt_round<2, true>(sh, tabs.sm, ns, logC, lsb);
-    if (rem == 1) ntt_round<1, true>(sh, tabs.sm, ns, logC, lsb);
-  } else {
-    uint32_t lsb = ns;
-    for (uint32_t i = 0; i < full; i++) {
-      lsb -= NTT_R;
-      ntt_round<NTT_R, false>(sh, tabs.sm, ns, logC, lsb);
-      __syncthreads();
-    }
-    if (rem == 2) ntt_round<2, false>(sh, tabs.sm, ns, logC, 0);
-    if (rem == 1) ntt_round<1, false>(sh, tabs.sm, ns, logC, 0);
-  }
-  __syncthreads();
+  ntt_rounds<DIT>(sh, tabs.sm, ns, logC);
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) {
     const uint32_t r = k >> logC, c = k & (C - 1);
     Fr v = ld_vec(&sh[k]);
@@ -129,14 +157,14 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(Fr* __restrict__ data,
 }
 
 static void run_pass(bool dit, Fr* d, const NttTabs& t, uint32_t log_n, uint32_t s_lo, uint32_t ns,
-                     hipStream_t st) {
+                     hipStream_t st, const Fr* src = nullptr, const Fr* ltab = nullptr) {
   const uint32_t logC = std::min<uint32_t>(s_lo, NTT_TILE_LOG - ns);
   const uint32_t tiles = (uint32_t)((1ull << log_n) >> (ns + logC));
   const size_t lds = sizeof(Fr) << (ns + logC);
   if (dit)
-    k_ntt_pass<true><<<tiles, NTT_THREADS, lds, st>>>(d, t, log_n, s_lo, ns, logC);
+    k_ntt_pass<true><<<tiles, NTT_THREADS, lds, st>>>(d, src ? src : d, ltab, t, log_n, s_lo, ns, logC);
   else
-    k_ntt_pass<false><<<tiles, NTT_THREADS, lds, st>>>(d, t, log_n, s_lo, ns, logC);
+    k_ntt_pass<false><<<tiles, NTT_THREADS, lds, st>>>(d, src ? src : d, ltab, t, log_n, s_lo, ns, logC);
   ZK_LAUNCH_CHECK();
 }
 
@@ -156,14 +184,16 @@ static std::vector<uint32_t> pass_plan(uint32_t L) {
 }
 
 
-void ntt_dif(Fr* d, const NttDomain& dom, bool inv, hipStream_t st, Prof* pf) {
+void ntt_dif(Fr* d, const NttDomain& dom, bool inv, hipStream_t st, Prof* pf, const Fr* src, const Fr* ltab) {
   const uint32_t L = dom.log_n;
   if (L == 0) return;
   const int ph = pf ? pf->begin(st, "ntt", (uint64_t)1 << L) : -1;
   const NttTabs t = tabs_of(dom, inv);
   uint32_t s_hi = L;
+  bool first = true;
   for (uint32_t ns : pass_plan(L)) {
-    run_pass(false, d, t, L, s_hi - ns, ns, st);
+    run_pass(false, d, t, L, s_hi - ns, ns, st, first ? src : nullptr, first ? ltab : nullptr);
+    first = false;
     s_hi -= ns;
   }
   if (pf) pf->end(st, ph);
@@ -199,29 +229,13 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_tile_shift(Fr* __restrict__
   const size_t base = (size_t)blockIdx.x << ns;
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) st_vec(&sh[k], ld_vec(&data[base + k]));
   __syncthreads();
-  const uint32_t full = ns / NTT_R, rem = ns % NTT_R;
-  uint32_t lsb = ns;
-  for (uint32_t i = 0; i < full; i++) {
-    lsb -= NTT_R;
-    ntt_round<NTT_R, false>(sh, ism, ns, 0, lsb);
-    __syncthreads();
-  }
-  if (rem == 2) ntt_round<2, false>(sh, ism, ns, 0, 0);
-  if (rem == 1) ntt_round<1, false>(sh, ism, ns, 0, 0);
-  __syncthreads();
+  ntt_rounds<false>(sh, ism, ns, 0);
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) {
     const uint32_t p = (uint32_t)(base + k);
     st_vec(&sh[k], fp_mul(ld_vec(&sh[k]), ld_vec(&tab[bitrev32(p, log_n)])));
   }
   __syncthreads();
-  lsb = 0;
-  for (uint32_t i = 0; i < full; i++, lsb += NTT_R) {
-    ntt_round<NTT_R, true>(sh, sm, ns, 0, lsb);
-    __syncthreads();
-  }
-  if (rem == 2) ntt_round<2, true>(sh, sm, ns, 0, lsb);
-  if (rem == 1) ntt_round<1, true>(sh, sm, ns, 0, lsb);
-  __syncthreads();
+  ntt_rounds<true>(sh, sm, ns, 0);
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) st_vec(&data[base + k], ld_vec(&sh[k]));
 }
 
@@ -369,6 +383,53 @@ __global__ void __launch_bounds__(256) k_scale_const(Fr* __restrict__ d, Fr c, s
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   st_vec(&d[i], fp_mul(ld_vec(&d[i]), c));
+}
+
+// Bit-reversal permutation through 32 x 32 LDS tiles: with i = x 2^(L-5) +
+// mid 2^5 + y, bitrev(i) = rev5(y) 2^(L-5) + rev(mid) 2^5 + rev5(x), so for a
+// fixed mid the 32 x 32 block (x, y) lands transposed at (rev5(y), rev5(x)):
+// both the 32-element rows read and the 32-element rows written are
+// contiguous (1 KiB).  Optional factor per output element.
+constexpr int BR_T = 5;
+__device__ __forceinline__ uint32_t rev5(uint32_t v) { return __builtin_bitreverse32(v) >> 27; }
+__global__ void __launch_bounds__(256) k_bitrev_tiled(const Fr* __restrict__ in, Fr* __restrict__ out, uint32_t L,
+                                                      const Fr* __restrict__ tab, Fr c, int mode) {
+  __shared__ Fr t[32 * 33];
+  const uint32_t mid = blockIdx.x, midbits = L - 2 * BR_T;
+  const uint32_t rmid = midbits ? (__builtin_bitreverse32(mid) >> (32 - midbits)) : 0;
+  for (uint32_t k = threadIdx.x; k < 1024; k += 256) {
+    const uint32_t x = k >> 5, y = k & 31;
+    const size_t i = ((size_t)x << (L - BR_T)) | ((size_t)mid << BR_T) | y;
+    t[x * 33 + y] = ld_vec(&in[i]);
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < 1024; k += 256) {
+    const uint32_t yr = k >> 5, xr = k & 31;
+    const size_t j = ((size_t)yr << (L - BR_T)) | ((size_t)rmid << BR_T) | xr;
+    Fr v = t[rev5(xr) * 33 + rev5(yr)];
+    if (mode == 1) v = fp_mul(v, ld_vec(&tab[j]));
+    else if (mode == 2) v = fp_mul(v, c);
+    st_vec(&out[j], v);
+  }
+}
+__global__ void __launch_bounds__(256) k_bitrev_small(const Fr* __restrict__ in, Fr* __restrict__ out, uint32_t L,
+                                                      const Fr* __restrict__ tab, Fr c, int mode) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >> L) return;
+  const uint32_t j = bitrev32(i, L);
+  Fr v = ld_vec(&in[i]);
+  if (mode == 1) v = fp_mul(v, ld_vec(&tab[j]));
+  else if (mode == 2) v = fp_mul(v, c);
+  st_vec(&out[j], v);
+}
+void fr_bitrev_scale(const Fr* in, Fr* out, uint32_t log_n, const Fr* tab, const Fr* c, hipStream_t st) {
+  const int mode = tab ? 1 : c ? 2 : 0;
+  const Fr cv = c ? *c : Fr{};
+  if (log_n >= 2 * BR_T)
+    k_bitrev_tiled<<<1u << (log_n - 2 * BR_T), 256, 0, st>>>(in, out, log_n, tab, cv, mode);
+  else
+    k_bitrev_small<<<ceil_div((size_t)1 << log_n, 256), 256, 0, st>>>(in, out, log_n, tab, cv, mode);
+  ZK_LAUNCH_CHECK();
 }
 
 void fr_to_mont(const uint64_t* d_canon, Fr* d_out, size_t n, hipStream_t st) {

@@ -62,7 +62,10 @@ inline NttTabs tabs_of(const NttDomain& dom, bool inv) {
 
 
 // In-place passes over n Montgomery Fr.
-void ntt_dif(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st, Prof* pf = nullptr);
+// ntt_dif's first pass may read `src` instead of d_data (out of place) and
+// multiply each loaded element by ltab[i] (natural index), e.g. a coset's g^i.
+void ntt_dif(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st, Prof* pf = nullptr,
+             const Fr* src = nullptr, const Fr* ltab = nullptr);
 void ntt_dit(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st, Prof* pf = nullptr);
 
 // d <- NTT(tab[bitrev(i)] * iNTT(d)) with the inverse DIF's last pass, the
@@ -76,6 +79,10 @@ void fr_from_mont(const Fr* d_in, uint64_t* d_canon, size_t n, hipStream_t st);
 void fr_scale_table(Fr* d_data, const Fr* d_tab, uint32_t log_n, bool bitrev, hipStream_t st);
 // out[i] = in[bitrev(i)] (out-of-place)
 void fr_bitrev_copy(const Fr* d_in, Fr* d_out, uint32_t log_n, hipStream_t st);
+// out[bitrev(i)] = in[i] * f, f = tab[bitrev(i)] (tab != nullptr), else c
+// (use_c), else 1: the natural-order permutation after a DIF transform,
+// tiled through LDS so reads and writes stay coalesced (log_n >= 10)
+void fr_bitrev_scale(const Fr* d_in, Fr* d_out, uint32_t log_n, const Fr* tab, const Fr* c, hipStream_t st);
 // data[i] *= c (Montgomery constant)
 void fr_scale_const(Fr* d_data, const Fr& c_host, size_t n, hipStream_t st);
 // out[i] = base^i * scale (Montgomery), i < n

@@ -1,0 +1,74 @@
+// host_san_check.cpp -- the host-side C++ of libzkp_amd.so (host_ec.hpp:
+// Fq/Fq2/XYZZ and scalar multiplication used by the MSM tails and the
+// s*pi_A + r*B1 term; host_pairing.hpp: the verifier's optimal-ate pairing)
+// under AddressSanitizer + UndefinedBehaviorSanitizer, host only
+// (tests/test_sanitizers.py builds it with g++).  Checks group-law and
+// bilinearity identities so the run is meaningful without a report.
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../zero-knowledge-proofs_amd/csrc/host_pairing.hpp"
+
+using namespace zk::host;
+
+static X<Fq> g1() {
+  X<Fq> p;
+  std::memcpy(p.X_.l, G1_GEN_HOSTM, 48);
+  std::memcpy(p.Y.l, G1_GEN_HOSTM + 12, 48);
+  p.ZZ = one();
+  p.ZZZ = one();
+  return p;
+}
+static X<Fq2> g2() {
+  X<Fq2> p;
+  std::memcpy(p.X_.c0.l, G2_GEN_HOSTM, 48);
+  std::memcpy(p.X_.c1.l, G2_GEN_HOSTM + 12, 48);
+  std::memcpy(p.Y.c0.l, G2_GEN_HOSTM + 24, 48);
+  std::memcpy(p.Y.c1.l, G2_GEN_HOSTM + 36, 48);
+  p.ZZ = f_one<Fq2>();
+  p.ZZZ = f_one<Fq2>();
+  return p;
+}
+template <class F>
+static bool same(const X<F>& a, const X<F>& b) {
+  F ax, ay, bx, by;
+  const bool ia = !to_affine(a, ax, ay), ib = !to_affine(b, bx, by);
+  if (ia || ib) return ia == ib;
+  return std::memcmp(&ax, &bx, sizeof ax) == 0 && std::memcmp(&ay, &by, sizeof ay) == 0;
+}
+
+int main() {
+  const uint64_t k1[4] = {0x1234567890abcdefull, 0x1111, 0, 0}, k2[4] = {0xfedcba987654321ull, 0, 7, 0};
+  uint64_t k12[4] = {0};
+  // (k1 + k2) P == k1 P + k2 P, in G1 and G2, and the Straus double multiplication
+  unsigned __int128 c = 0;
+  for (int i = 0; i < 4; i++) {
+    c += (unsigned __int128)k1[i] + k2[i];
+    k12[i] = (uint64_t)c;
+    c >>= 64;
+  }
+  const auto P = g1();
+  const auto Q = g2();
+  if (!same(mul_scalar(P, k12), addp(mul_scalar(P, k1), mul_scalar(P, k2)))) return 1;
+  if (!same(mul_scalar(Q, k12), addp(mul_scalar(Q, k1), mul_scalar(Q, k2)))) return 2;
+  if (!same(mul2_scalar(P, k1, P, k2), mul_scalar(P, k12))) return 3;
+  if (!same(dbl(P), addp(P, P))) return 4;
+  // bilinearity: e(k1 P, Q) e(-P, k1 Q) == 1
+  Fq px, py, qx0, qy0;
+  Fq2 qx, qy, rx, ry;
+  to_affine(mul_scalar(P, k1), px, py);
+  to_affine(Q, qx, qy);
+  to_affine(mul_scalar(Q, k1), rx, ry);
+  Fq gx, gy;
+  to_affine(P, gx, gy);
+  std::vector<A1> ps = {A1{px, py, false}, A1{gx, neg(gy), false}};
+  std::vector<A2> qs = {A2{qx, qy, false}, A2{rx, ry, false}};
+  if (!pairing_product_is_one(ps, qs)) return 5;
+  qs[1] = A2{qx, qy, false};
+  if (pairing_product_is_one(ps, qs)) return 6;
+  (void)qx0;
+  (void)qy0;
+  std::printf("host sanitizer check ok\n");
+  return 0;
+}

@@ -98,7 +98,23 @@ struct Prof {
     std::string phase;
     hipEvent_t a, b;
     uint64_t units;
+    hipStream_t st;
   };
+  // Timeline (tuning): with ZK_TIMELINE=<file>, collect() appends one line
+  // per phase -- name, stream, start and end in ms after the last
+  // mark_origin() -- so an unprofiled run shows how the streams overlap.
+  hipEvent_t origin = nullptr;
+  bool origin_set = false;
+  const char* timeline_path() {
+    static const char* p = getenv("ZK_TIMELINE");
+    return p;
+  }
+  void mark_origin(hipStream_t st) {
+    if (!on || !timeline_path()) return;
+    if (!origin) ZK_HIP(hipEventCreate(&origin));
+    ZK_HIP(hipEventRecord(origin, st));
+    origin_set = true;
+  }
   std::vector<Rec> pending;
   std::vector<hipEvent_t> pool;
   std::map<std::string, PhaseStat> stats;
@@ -116,7 +132,7 @@ struct Prof {
   // returns an index to close with end(); -1 when disabled
   int begin(hipStream_t st, const char* phase, uint64_t units) {
     if (!on) return -1;
-    Rec r{phase, ev(), ev(), units};
+    Rec r{phase, ev(), ev(), units, st};
     ZK_HIP(hipEventRecord(r.a, st));
     pending.push_back(r);
     return (int)pending.size() - 1;
@@ -134,10 +150,17 @@ struct Prof {
   }
   // after the stream has been synchronised
   void collect() {
+    FILE* tl = (origin_set && timeline_path()) ? fopen(timeline_path(), "a") : nullptr;
     for (Rec& r : pending) {
       float ms = 0;
       ZK_HIP(hipEventSynchronize(r.b));
       ZK_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+      if (tl) {
+        float t0 = 0, t1 = 0;
+        ZK_HIP(hipEventElapsedTime(&t0, origin, r.a));
+        ZK_HIP(hipEventElapsedTime(&t1, origin, r.b));
+        fprintf(tl, "%s %p %.4f %.4f\n", r.phase.c_str(), (void*)r.st, t0, t1);
+      }
       PhaseStat& s = stats[r.phase];
       s.ms += ms;
       s.launches += 1;
@@ -146,8 +169,14 @@ struct Prof {
       pool.push_back(r.b);
     }
     pending.clear();
+    if (tl) {
+      fprintf(tl, "--\n");
+      fclose(tl);
+    }
+    origin_set = false;
   }
   ~Prof() {
+    if (origin) (void)hipEventDestroy(origin);
     for (Rec& r : pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     for (hipEvent_t e : pool) (void)hipEventDestroy(e);
   }

@@ -977,6 +977,9 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
   // The number of non-zero digits M' <= M is known on device only: the T
   // accumulate threads split it evenly there (chunk_len), no host sync.
   if (M) {
+    // the accumulate may be held until another stream's event (the prove's
+    // quotient): its full-occupancy round would otherwise starve that work
+    if (w.accum_wait) ZK_HIP(hipStreamWaitEvent(st, w.accum_wait, 0));
     ph = pf ? pf->begin(st, (w.tag + (g2 ? "msm_accum_g2" : "msm_accum_g1")).c_str(), n) : -1;
     // ZK_MSM_IDXMASK (experiment only, wrong results): confine the base
     // gathers to a cache-resident prefix to measure the kernel without HBM

@@ -94,6 +94,7 @@ struct MsmWork {
   PinnedBuf host_res;
   MsmPlan plan{};
   Prof* prof = nullptr;  // optional live kernel timing
+  hipEvent_t accum_wait = nullptr;   // if set, the accumulate kernel waits for this event
   std::string tag;       // phase-name prefix (per-MSM profiling)
 };
 

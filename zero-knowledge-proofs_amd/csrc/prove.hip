@@ -404,6 +404,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   const auto t_start = clk::now();
   hipStream_t st = ctx->stream;
   ctx->flags.ensure(16);
+  ctx->prof.mark_origin(st);
   const int ph_span = ctx->prof.begin(st, "prove_gpu_span", pk->n);   // first kernel .. last MSM done
   ZK_HIP(hipMemsetAsync(ctx->flags.p, 0, 16, st));
   check_canonical(d_z, pk->V, ctx->flags.as<uint32_t>(), st);   // every z_i < r, else ZK_ERR_ARG
@@ -536,8 +537,18 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
     };
     auto has_h = [](const std::vector<int>& grp) { return std::find(grp.begin(), grp.end(), (int)MSM_H) != grp.end(); };
     // ZK_PROVE_SCHED=4: the quotient's kernels are queued first (host launch
-    // order only, no waits), then the G2 MSM and the groups
-    if (sched == 4) run_quotient();
+    // order only, no waits), then the G2 MSM and the groups.  5: the same,
+    // and the side streams' accumulate kernels wait for the quotient (their
+    // key and sort passes still overlap it): a full-occupancy accumulate
+    // round otherwise holds every SIMD's registers and starves the
+    // quotient's LDS-tiled NTT passes, which delays the H MSM behind it.
+    if (sched == 4 || sched == 5) run_quotient();
+    if (sched == 5) {
+      ZK_HIP(hipEventRecord(ctx->ev_quot, st));
+      for (int sl = 0; sl < NUM_MSM; sl++) ctx->msm[sl].accum_wait = sl == MSM_H ? nullptr : ctx->ev_quot;
+    } else {
+      for (int sl = 0; sl < NUM_MSM; sl++) ctx->msm[sl].accum_wait = nullptr;
+    }
     if (sched == 3) {
       launch_slot(MSM_B2, st);
     } else if (sched != 1) {
@@ -558,7 +569,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       }
       launch_group(grp, gs);
     }
-    if (sched != 4) run_quotient();
+    if (sched != 4 && sched != 5) run_quotient();
     if (sched == 1) {
       ZK_HIP(hipEventRecord(ctx->ev_quot, st));
       ZK_HIP(hipStreamWaitEvent(s2, ctx->ev_quot, 0));
@@ -642,6 +653,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   }
   for (int k = 0; k < NUM_SIDE; k++) ZK_HIP(hipStreamSynchronize(ctx->side[k]));
   ZK_HIP(hipStreamSynchronize(st));
+  for (int sl = 0; sl < NUM_MSM; sl++) ctx->msm[sl].accum_wait = nullptr;
   ctx->prof.add_host("host_finish", t_fin);
   ctx->prof.collect();
   const uint32_t flags = h_given ? given_flags : *ctx->flags_host.as<uint32_t>();

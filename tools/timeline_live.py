@@ -34,8 +34,9 @@ def main():
         os.remove(path)
     ctx.profile(True)
     for _ in range(4):
-        zkp.Prover.prove_device(dpk, z.data_ptr(), 3 * n + 1, 1, r, s)
+        pr = zkp.Prover.prove_device(dpk, z.data_ptr(), 3 * n + 1, 1, r, s)
     ctx.profile(False)
+    print("proof b:", pr.serialize_compressed().hex()[96:140], "phases:", sorted(ctx.profile_read().keys()) if False else "")
     blocks = [b for b in open(path).read().strip().split("--") if b.strip()]
     for bi, blk in enumerate(blocks[-2:]):
         lines = [ln.split() for ln in blk.strip().splitlines() if ln.strip()]

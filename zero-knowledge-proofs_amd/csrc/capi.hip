@@ -62,6 +62,7 @@ zk_ctx* zk_ctx_create(int device) {
     for (int i = 1; i < NUM_SIDE; i++) ZK_HIP(hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking, lo_prio));
     ZK_HIP(hipEventCreateWithFlags(&c->ev_quot, hipEventDisableTiming));
     ZK_HIP(hipEventCreateWithFlags(&c->ev_scal, hipEventDisableTiming));
+    ZK_HIP(hipEventCreateWithFlags(&c->ev_hsort, hipEventDisableTiming));
     for (auto& e : c->ev_done) ZK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     return c.release();
   } catch (...) {
@@ -79,6 +80,7 @@ void zk_ctx_destroy(zk_ctx* ctx) {
   (void)hipStreamDestroy(ctx->stream);
   (void)hipEventDestroy(ctx->ev_quot);
   (void)hipEventDestroy(ctx->ev_scal);
+  (void)hipEventDestroy(ctx->ev_hsort);
   for (auto& e : ctx->ev_done) (void)hipEventDestroy(e);
   delete ctx;
 }

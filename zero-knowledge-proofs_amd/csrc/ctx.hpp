@@ -29,7 +29,7 @@ struct zk_ctx {
   int device = 0;
   hipStream_t stream = nullptr;                 // main stream
   hipStream_t side[zk::NUM_SIDE] = {};          // G2 / IC / A+B1 MSM streams
-  hipEvent_t ev_quot = nullptr, ev_scal = nullptr;
+  hipEvent_t ev_quot = nullptr, ev_scal = nullptr, ev_hsort = nullptr;
   hipEvent_t ev_done[zk::NUM_MSM] = {};         // per-MSM completion (results downloaded)
   std::string err;
   zk::MsmWork msm[zk::NUM_MSM];

@@ -974,6 +974,7 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
     }
   }
   if (pf) pf->end(st, ph);
+  if (w.sort_done) ZK_HIP(hipEventRecord(w.sort_done, st));   // the grouping is done
   // The number of non-zero digits M' <= M is known on device only: the T
   // accumulate threads split it evenly there (chunk_len), no host sync.
   if (M) {

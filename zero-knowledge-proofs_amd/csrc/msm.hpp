@@ -95,6 +95,7 @@ struct MsmWork {
   MsmPlan plan{};
   Prof* prof = nullptr;  // optional live kernel timing
   hipEvent_t accum_wait = nullptr;   // if set, the accumulate kernel waits for this event
+  hipEvent_t sort_done = nullptr;    // if set, recorded once the entries are grouped by bucket
   std::string tag;       // phase-name prefix (per-MSM profiling)
 };
 

@@ -130,7 +130,12 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(Fr* __restrict__ data,
   const uint32_t C = 1u << logC;
   const uint32_t tile_elems = (1u << ns) << logC;
   const uint32_t lo_blocks = (1u << s_lo) >> logC;      // column blocks per hi
-  const uint32_t tile = blockIdx.x;
+  // XCD-aware order: workgroups go round-robin to the 8 XCDs, so XCD x gets
+  // the contiguous tile range [x G/8, (x+1) G/8) -- neighbouring column
+  // blocks (which share 128-byte lines when tiles are 1-2 columns wide) meet
+  // in one XCD's L2
+  const uint32_t G = gridDim.x;
+  const uint32_t tile = (G & 7) ? blockIdx.x : (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
   const uint32_t hi = tile / lo_blocks;
   const uint32_t lo0 = (tile % lo_blocks) << logC;
   const size_t base = ((size_t)hi << (s_lo + ns)) + lo0;
@@ -170,13 +175,22 @@ static void run_pass(bool dit, Fr* d, const NttTabs& t, uint32_t log_n, uint32_t
 
 // Pass plan, top (first DIF pass) to bottom: the contiguous pass (s_lo = 0)
 // takes up to 11 stages; the rest are split evenly into strided passes of
-// <= 9 stages, so tiles keep >= 4 consecutive columns (128-byte rows).
+// <= ZK_NTT_MAXSTRIDED stages (default 9: tiles keep >= 4 consecutive
+// columns, 128-byte rows).
+static uint32_t max_strided() {
+  static const uint32_t v = [] {
+    const char* e = getenv("ZK_NTT_MAXSTRIDED");
+    return e ? (uint32_t)std::max(1, std::min(NTT_TILE_LOG, atoi(e))) : (uint32_t)(NTT_TILE_LOG - 2);
+  }();
+  return v;
+}
 static std::vector<uint32_t> pass_plan(uint32_t L) {
   const uint32_t last = std::min<uint32_t>(L, NTT_TILE_LOG);
   const uint32_t rest = L - last;
   std::vector<uint32_t> ns;
   if (rest) {
-    const uint32_t np = (rest + (NTT_TILE_LOG - 2) - 1) / (NTT_TILE_LOG - 2);
+    const uint32_t ms = max_strided();
+    const uint32_t np = (rest + ms - 1) / ms;
     for (uint32_t i = 0; i < np; i++) ns.push_back(rest / np + (i < rest % np ? 1 : 0));
   }
   ns.push_back(last);

@@ -542,13 +542,32 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
     // key and sort passes still overlap it): a full-occupancy accumulate
     // round otherwise holds every SIMD's registers and starves the
     // quotient's LDS-tiled NTT passes, which delays the H MSM behind it.
-    if (sched == 4 || sched == 5) run_quotient();
+    // 6: the H group's key and sort passes also go ahead (queued right
+    // after the quotient on the main stream) and every accumulate waits for
+    // them -- sorts and the quotient share the chip, the accumulates start
+    // together once every MSM's entries are grouped.
+    for (int sl = 0; sl < NUM_MSM; sl++) {
+      ctx->msm[sl].accum_wait = nullptr;
+      ctx->msm[sl].sort_done = nullptr;
+    }
+    if (sched == 4 || sched == 5 || sched == 6) run_quotient();
     if (sched == 5) {
       ZK_HIP(hipEventRecord(ctx->ev_quot, st));
       for (int sl = 0; sl < NUM_MSM; sl++) ctx->msm[sl].accum_wait = sl == MSM_H ? nullptr : ctx->ev_quot;
-    } else {
-      for (int sl = 0; sl < NUM_MSM; sl++) ctx->msm[sl].accum_wait = nullptr;
     }
+    if (sched == 6) {
+      ctx->flags_host.ensure(16);
+      ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
+      for (const auto& grp : groups)
+        if (has_h(grp)) {
+          ctx->msm[grp[0]].sort_done = ctx->ev_hsort;
+          launch_group(grp, st);
+        }
+      for (int sl = 0; sl < NUM_MSM; sl++) ctx->msm[sl].accum_wait = ctx->ev_hsort;
+      for (const auto& grp : groups)
+        if (has_h(grp)) ctx->msm[grp[0]].accum_wait = nullptr;
+    }
+    // the G2 MSM starts with the witness (ZK_PROVE_SCHED=1: after the quotient, below)
     if (sched == 3) {
       launch_slot(MSM_B2, st);
     } else if (sched != 1) {
@@ -569,7 +588,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       }
       launch_group(grp, gs);
     }
-    if (sched != 4 && sched != 5) run_quotient();
+    if (sched != 4 && sched != 5 && sched != 6) run_quotient();
     if (sched == 1) {
       ZK_HIP(hipEventRecord(ctx->ev_quot, st));
       ZK_HIP(hipStreamWaitEvent(s2, ctx->ev_quot, 0));
@@ -577,10 +596,12 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
     }
     ZK_HIP(hipEventRecord(ctx->ev_done[MSM_B2], s2));
     waits.push_back(MSM_B2);
-    ctx->flags_host.ensure(16);
-    ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
-    for (const auto& grp : groups)
-      if (has_h(grp)) launch_group(grp, st);
+    if (sched != 6) {
+      ctx->flags_host.ensure(16);
+      ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
+      for (const auto& grp : groups)
+        if (has_h(grp)) launch_group(grp, st);
+    }
     if (ph_span >= 0) {
       for (int sl : waits) ZK_HIP(hipStreamWaitEvent(st, ctx->ev_done[sl], 0));
       ctx->prof.end(st, ph_span);
@@ -653,7 +674,10 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   }
   for (int k = 0; k < NUM_SIDE; k++) ZK_HIP(hipStreamSynchronize(ctx->side[k]));
   ZK_HIP(hipStreamSynchronize(st));
-  for (int sl = 0; sl < NUM_MSM; sl++) ctx->msm[sl].accum_wait = nullptr;
+  for (int sl = 0; sl < NUM_MSM; sl++) {
+    ctx->msm[sl].accum_wait = nullptr;
+    ctx->msm[sl].sort_done = nullptr;
+  }
   ctx->prof.add_host("host_finish", t_fin);
   ctx->prof.collect();
   const uint32_t flags = h_given ? given_flags : *ctx->flags_host.as<uint32_t>();

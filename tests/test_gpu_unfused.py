@@ -1,4 +1,5 @@
-"""The unfused quotient path (ZK_NTT_FUSE=0: iNTT, separate n^-1 g^i scale,
+"""Non-default prover paths stay bit-exact, each in a child process (the
+switches are read once per process).  The unfused quotient path (ZK_NTT_FUSE=0: iNTT, separate n^-1 g^i scale,
 NTT) stays bit-exact: it is the fallback the fused tile kernel replaced and
 no other test runs it (the switch is read once per process, so a child
 process runs it).  Sizes cover 1 NTT pass (2^0 .. 2^11), 2 passes (2^12) and
@@ -16,7 +17,19 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 @pytest.mark.timeout(300)
 def test_unfused_quotient_matches_oracle():
     env = dict(os.environ, ZK_NTT_FUSE="0")
-    res = subprocess.run([sys.executable, os.path.join(HERE, "unfused_quotient_check.py"), "0", "1", "11", "12", "21"],
+    res = subprocess.run([sys.executable, os.path.join(HERE, "unfused_quotient_check.py"), "ZK_NTT_FUSE=0", "0", "1", "11",
+                          "12", "21"],
                          env=env, capture_output=True, text=True, timeout=280)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
     assert res.stdout.count(" ok") == 5
+
+
+@pytest.mark.timeout(300)
+def test_lazy_accumulate_matches_oracle():
+    """ZK_LAZY_ACCUM=1: the G1 bucket accumulate in csrc/lazy.hpp's redundant
+    signed-limb Fq form (an opt-in experiment) against the oracle."""
+    env = dict(os.environ, ZK_LAZY_ACCUM="1")
+    res = subprocess.run([sys.executable, os.path.join(HERE, "unfused_quotient_check.py"), "ZK_LAZY_ACCUM=1", "2", "10",
+                          "16"], env=env, capture_output=True, text=True, timeout=280)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
+    assert res.stdout.count(" ok") == 3

@@ -6,6 +6,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "lazy.hpp"
 #include "msm.hpp"
 
 namespace zk {
@@ -379,6 +380,76 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum(SegBases<typena
   else st_vec(&buckets[cur], acc);
 }
 
+// G1 accumulate in lazy.hpp's redundant Fq form: the same chunks, loop,
+// branches and flushes as k_msm_accum<G1>; the accumulator stays in signed
+// 28-bit limbs between adds and is made canonical only when flushed.
+ZK_DI void st_lazy(G1X* p, const FlX& a) {
+  st_vec(&p->X, fl_to_fq(a.X));
+  ZK_SB();
+  st_vec(&p->Y, fl_to_fq(a.Y));
+  ZK_SB();
+  st_vec(&p->ZZ, fl_to_fq(a.ZZ));
+  ZK_SB();
+  st_vec(&p->ZZZ, fl_to_fq(a.ZZZ));
+}
+#ifndef ZK_LAZY_WPE
+#define ZK_LAZY_WPE 3
+#endif
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(ZK_LAZY_WPE))) k_msm_accum_g1l(SegBases<G1A> sb, uint32_t segshift,
+                                                                    uint32_t idx_mask,
+                                                                    const uint32_t* __restrict__ ent,
+                                                                    const uint32_t* __restrict__ key,
+                                                                    const uint32_t* __restrict__ off, uint32_t G,
+                                                                    uint32_t T, G1X* __restrict__ buckets,
+                                                                    G1X* __restrict__ partials) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t M = off[G];
+  const uint32_t K = chunk_len(M, T);
+  const uint32_t start = t * K;
+  if (t >= T || start >= M) return;
+  const uint32_t end = min(start + K, M);
+  FlX acc;
+  flx_set_inf(acc);
+  uint32_t cur = key[start], run_start = start;
+  for (uint32_t e = start; e < end; e++) {
+    const uint32_t g = key[e];
+    const uint32_t en = ent[e];
+    if (g != cur) {
+      const bool head = (run_start == start) && (off[cur] < start);
+      st_lazy(head ? &partials[2 * (size_t)t] : &buckets[cur], acc);
+      flx_set_inf(acc);
+      cur = g;
+      run_start = e;
+    }
+    if (en == MSM_DUMMY) continue;
+    const uint32_t seg = g >> segshift;
+    const G1A* bases = sb.p[0];
+#pragma unroll
+    for (int k = 1; k < MSM_MAXSEG; k++)
+      if (seg == (uint32_t)k) bases = sb.p[k];
+    const G1A a = ld_vec(&bases[en & idx_mask]);
+    if (aff_is_inf(a)) continue;
+    FlA la{fl_from_fq(a.x), fl_from_fq(a.y)};
+    if (en & 0x80000000u) la.y = fl_neg(la.y);
+    acc = flx_madd(acc, la);
+  }
+  const bool head = (run_start == start) && (off[cur] < start);
+  const bool tail = off[cur + 1] > end;
+  st_lazy(head ? &partials[2 * (size_t)t] : tail ? &partials[2 * (size_t)t + 1] : &buckets[cur], acc);
+}
+// ZK_LAZY_ACCUM=1 selects k_msm_accum_g1l (experiment, off by default):
+// ~10% fewer VALU instructions per madd than k_msm_accum<G1>, but the
+// signed product columns need more registers (227 VGPRs unconstrained, 168
+// with 25 spilled at 3 waves/SIMD) and the prove is no faster (9.93 vs
+// 9.97 ms, 2 waves: 10.15 ms).
+static bool g1_lazy_mode() {
+  static const bool v = [] {
+    const char* e = getenv("ZK_LAZY_ACCUM");
+    return e && std::strcmp(e, "1") == 0;
+  }();
+  return v;
+}
+
 // G2 accumulate over lane pairs (Fq2h, ff.hpp): chunk t is owned by lanes
 // 2t, 2t+1, each holding one Fq coefficient of every Fq2 coordinate.  The
 // loop, its branches and the flushes are those of k_msm_accum; the pair's
@@ -655,6 +726,14 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_quant(MsmPlan p, con
 #ifndef ZK_RED_QWAVES
 #define ZK_RED_QWAVES 4
 #endif
+// the env variable of the same name overrides the build-time mask (A/B runs)
+static uint32_t red_quad_mask() {
+  static const uint32_t m = [] {
+    const char* e = getenv("ZK_RED_QUAD");
+    return e ? (uint32_t)strtoul(e, nullptr, 0) : (uint32_t)ZK_RED_QUAD;
+  }();
+  return m;
+}
 
 template <class X, int RW>
 __device__ __forceinline__ X quad_sum_step(X v, uint32_t it, uint32_t niter, X* xs, bool have, const X& term) {
@@ -869,6 +948,8 @@ static uint32_t accum_threads() {
     const bool pair = std::is_same<C, G2>::value && g2_pair_mode();   // two lanes per chunk
     if (pair)
       ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_accum_pair, 128, 0));
+    else if (std::is_same<C, G1>::value && g1_lazy_mode())
+      ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_accum_g1l, 128, 0));
     else
       ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_accum<C>, 128, 0));
     double rounds = 1.0;   // tuning: fractions leave room for concurrent streams
@@ -988,7 +1069,7 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
       const char* e = getenv("ZK_MSM_IDXMASK");
       return e ? (uint32_t)strtoul(e, nullptr, 0) & 0x7fffffffu : 0x7fffffffu;
     }();
-    bool pair = false;
+    bool pair = false, lazy = false;
     if constexpr (std::is_same<C, G2>::value) {
       pair = g2_pair_mode();
       if (pair)
@@ -996,7 +1077,15 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
             sb, p.segshift, idx_mask, w.ent.as<uint32_t>(), w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T,
             w.buckets.as<X>(), w.partials.as<X>());
     }
-    if (!pair)
+    if constexpr (std::is_same<C, G1>::value) {
+      if (g1_lazy_mode()) {
+        lazy = true;
+        k_msm_accum_g1l<<<ceil_div(p.T, 128), 128, 0, st>>>(sb, p.segshift, idx_mask, w.ent.as<uint32_t>(),
+                                                             w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T,
+                                                             w.buckets.as<X>(), w.partials.as<X>());
+      }
+    }
+    if (!pair && !lazy)
       k_msm_accum<C><<<ceil_div(p.T, 128), 128, 0, st>>>(sb, p.segshift, idx_mask, w.ent.as<uint32_t>(),
                                                           w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T,
                                                           w.buckets.as<X>(), w.partials.as<X>());
@@ -1010,7 +1099,7 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
     k_msm_fixup_pair<<<ceil_div(2 * (size_t)p.G, 128), 128, 0, st>>>(
         w.off.as<uint32_t>(), p.G, p.T, p.fix_max, w.nbig.as<uint32_t>(), reinterpret_cast<G2X*>(w.buckets.p),
         reinterpret_cast<const G2X*>(w.partials.p));
-  else if ((ZK_RED_QUAD & 4) && !g2)
+  else if ((red_quad_mask() & 4) && !g2)
     k_msm_fixup_q<C><<<ceil_div(4 * (size_t)p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), p.G, p.T, p.fix_max,
                                                                      w.nbig.as<uint32_t>(), w.buckets.as<X>(),
                                                                      w.partials.as<X>());
@@ -1039,13 +1128,13 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
   if (g2 && g2_pair_mode())
     k_msm_rowcol_pair<<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(
         p, w.off.as<uint32_t>(), reinterpret_cast<const G2X*>(w.buckets.p), reinterpret_cast<G2X*>(w.rc.p));
-  else if ((ZK_RED_QUAD & 2) || (!g2 && p.nrc <= rowcol_quad_max()))
+  else if ((red_quad_mask() & 2) || (!g2 && p.nrc <= rowcol_quad_max()))
     k_msm_rowcol_q<C, RW><<<p.nrc, 64 * RW, 0, st>>>(p, w.off.as<uint32_t>(), w.buckets.as<X>(), w.rc.as<X>());
   else
     k_msm_rowcol<C><<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.off.as<uint32_t>(),
                                                                                   w.buckets.as<X>(), w.rc.as<X>());
   ZK_LAUNCH_CHECK();
-  if (ZK_RED_QUAD & 1)
+  if (red_quad_mask() & 1)
     k_msm_quant_q<C, RW><<<p.nq, 64 * RW, 0, st>>>(p, w.rc.as<X>(), w.res.as<X>());
   else
     k_msm_quant<C><<<ceil_div(p.nq, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.rc.as<X>(), w.res.as<X>());

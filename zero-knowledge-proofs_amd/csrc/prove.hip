@@ -545,17 +545,19 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
     // 6: the H group's key and sort passes also go ahead (queued right
     // after the quotient on the main stream) and every accumulate waits for
     // them -- sorts and the quotient share the chip, the accumulates start
-    // together once every MSM's entries are grouped.
+    // together once every MSM's entries are grouped.  7: as 6, but the G2
+    // accumulate starts with the witness; only the batched G1 accumulates
+    // wait for the H group's sort.
     for (int sl = 0; sl < NUM_MSM; sl++) {
       ctx->msm[sl].accum_wait = nullptr;
       ctx->msm[sl].sort_done = nullptr;
     }
-    if (sched == 4 || sched == 5 || sched == 6) run_quotient();
+    if (sched >= 4 && sched <= 7) run_quotient();
     if (sched == 5) {
       ZK_HIP(hipEventRecord(ctx->ev_quot, st));
       for (int sl = 0; sl < NUM_MSM; sl++) ctx->msm[sl].accum_wait = sl == MSM_H ? nullptr : ctx->ev_quot;
     }
-    if (sched == 6) {
+    if (sched == 6 || sched == 7) {
       ctx->flags_host.ensure(16);
       ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
       for (const auto& grp : groups)
@@ -566,6 +568,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       for (int sl = 0; sl < NUM_MSM; sl++) ctx->msm[sl].accum_wait = ctx->ev_hsort;
       for (const auto& grp : groups)
         if (has_h(grp)) ctx->msm[grp[0]].accum_wait = nullptr;
+      if (sched == 7) ctx->msm[MSM_B2].accum_wait = nullptr;
     }
     // the G2 MSM starts with the witness (ZK_PROVE_SCHED=1: after the quotient, below)
     if (sched == 3) {
@@ -588,7 +591,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       }
       launch_group(grp, gs);
     }
-    if (sched != 4 && sched != 5 && sched != 6) run_quotient();
+    if (sched < 4 || sched > 7) run_quotient();
     if (sched == 1) {
       ZK_HIP(hipEventRecord(ctx->ev_quot, st));
       ZK_HIP(hipStreamWaitEvent(s2, ctx->ev_quot, 0));
@@ -596,7 +599,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
     }
     ZK_HIP(hipEventRecord(ctx->ev_done[MSM_B2], s2));
     waits.push_back(MSM_B2);
-    if (sched != 6) {
+    if (sched != 6 && sched != 7) {
       ctx->flags_host.ensure(16);
       ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
       for (const auto& grp : groups)

@@ -170,12 +170,14 @@ def pmc_prove(fetch_db, write_db, out, factor):
                for k, (n, fb, wb) in sorted(agg.items())}
     acc = [(fv * 1024, wv * 1024) for (_, k, fv), (_, _, wv) in zip(fd, wd) if "k_msm_accum" in k and "pair" not in k]
     res = {"note": f"serial prove (ZK_PROVE_SCHED=3); traffic_calibrated = {factor} x FETCH_SIZE + WRITE_SIZE "
-                   "(FETCH factor from tools/gather_calib for 96-byte gathers, profiles/r02_fetch_calibration.json); "
-                   "traffic_guide_2x = the guide's streaming correction",
+                   "(FETCH factor from tools/gather_calib for the accumulate's gather shape -- 1.779 for 96-byte "
+                   "points read at a 128-byte stride (k_gather<6,8>), 1.585 for packed 96-byte points -- "
+                   "profiles/r02_fetch_calibration.json); traffic_guide_2x = the guide's streaming correction",
            "kernels": kernels}
     if acc:
-        big = [a for a in acc if a[0] > 2e9]
-        small = [a for a in acc if a[0] <= 2e9]
+        cut = max(f for f, _ in acc) / 2   # the A+B1+IC batch launch vs the H launch of each prove
+        big = [a for a in acc if a[0] > cut]
+        small = [a for a in acc if a[0] <= cut]
         per = lambda L: int(sum(factor * f + w for f, w in L) / len(L)) if L else None
         res["msm_accum_g1_abi_bytes_per_launch"] = per(big)
         res["msm_accum_g1_h_bytes_per_launch"] = per(small)

@@ -230,6 +230,7 @@ static int msm_upload(zk_ctx* ctx, const ABI* bases, size_t n, int group, uint32
       ZK_HIP(hipMemcpyAsync(raw.p, bases, sizeof(ABI) * n, hipMemcpyHostToDevice, ctx->stream));
       convert_bases<C>(raw.as<uint64_t>(), b->bases.as<typename C::A>(), n, ctx->stream);
       if (W > 1) msm_precompute_windows<C>(b->bases.as<typename C::A>(), n, W, MSM_UPLOAD_WIN_C, ctx->stream);
+      b->stride = msm_pad_bases<C>(b->bases, n * W, ctx->stream);
     }
     if (W > 1) {
       b->win = W;
@@ -298,9 +299,9 @@ static int msm_dev(zk_ctx* ctx, const zk_msm_bases* b, const void* d_sc, size_t 
     MsmWork& w = ctx->msm[0];
     const int mbits = sw == 1 ? 64 : 255;
     if (b->win > 1 && (uint32_t)mbits <= b->win_bits)   // one bucket set over the shifted copies
-      msm_launch_shared<C>(w, b->bases.as<typename C::A>(), sc, sw, (uint32_t)n, mbits, b->win_c, st);
+      msm_launch_shared<C>(w, b->bases.as<typename C::A>(), sc, sw, (uint32_t)n, mbits, b->win_c, st, b->stride);
     else
-      msm_launch<C>(w, b->bases.as<typename C::A>(), sc, sw, (uint32_t)n, mbits, st);
+      msm_launch<C>(w, b->bases.as<typename C::A>(), sc, sw, (uint32_t)n, mbits, st, b->stride);
     msm_download<C>(w, st);
     ZK_HIP(hipStreamSynchronize(st));
     ctx->prof.collect();

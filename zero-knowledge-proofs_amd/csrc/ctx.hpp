@@ -62,6 +62,9 @@ struct zk_pk_dev {
   // Window-shifted base copies (msm_precompute_windows): bases[slot] holds
   // win x (count + extras) points, window w = 2^(win_c w) x the base.
   int win = 1, win_c = 0;
+  // Bytes between consecutive bases of bases[slot]: 0 = packed (sizeof the
+  // affine point), else padded to whole 128-B lines (msm_pad_bases).
+  uint32_t stride[zk::NUM_MSM] = {};
 };
 
 namespace zk {
@@ -81,4 +84,5 @@ struct zk_msm_bases {
   zk::DevBuf bases;   // n points, or win x n window-shifted copies (window-major)
   int win = 1, win_c = 0;
   uint32_t win_bits = 0;   // scalars up to this width use the shared bucket set
+  uint32_t stride = 0;     // bytes between bases (0 = packed), see msm_pad_bases
 };

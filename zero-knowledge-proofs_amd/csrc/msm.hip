@@ -317,7 +317,45 @@ __global__ void __launch_bounds__(256) k_scan_down(uint32_t* __restrict__ counts
 // over the T accumulate threads, T = one full-occupancy wave set of the
 // chip, so every launch is exactly one balanced round whatever the digit
 // distribution.
-__device__ __forceinline__ uint32_t chunk_len(uint32_t M, uint32_t T) { return M ? (M + T - 1) / T : 1u; }
+// K is a multiple of 4: EntQ's 16-byte loads stay aligned.
+__device__ __forceinline__ uint32_t chunk_len(uint32_t M, uint32_t T) {
+  return M ? ((M + T - 1) / T + 3) / 4 * 4 : 4u;
+}
+
+// The sorted (key, entry) pairs of a chunk, fetched ENTQ at a time with
+// 16-byte loads into the lane's own column of an LDS slab (no sharing, so
+// no barriers: LDS only extends the registers, which the accumulate has
+// none of to spare at 3 waves/SIMD).  A chunk is contiguous but a wave's 64
+// lanes are K entries apart, so one 4-byte load per entry touches 64 lines
+// per wave per entry, and the lines a full-occupancy round keeps open per
+// XCD (~6 MB) outgrow its 4 MB L2: each line came back from the fabric up to
+// 32 times; now at most 128 B / (4 B x ENTQ) = 2.  Reads may run ENTQ - 1
+// entries past the chunk (the arrays carry that slack).
+constexpr uint32_t ENTQ = 16;
+constexpr uint32_t ENTQ_LDS_WORDS = 2 * ENTQ * 64;   // per wave
+struct EntQ {
+  uint32_t* col;   // this lane's column: keys at col[64 j], entries at col[64 (ENTQ + j)]
+  ZK_DI explicit EntQ(uint32_t* lds) : col(lds + (threadIdx.x >> 6) * ENTQ_LDS_WORDS + (threadIdx.x & 63)) {}
+  // entry i = start, start + 1, ... in order (the refill is uniform across the wave)
+  ZK_DI void next(const uint32_t* __restrict__ key, const uint32_t* __restrict__ ent, uint32_t start, uint32_t i,
+                  uint32_t& g, uint32_t& en) {
+    const uint32_t j = (i - start) & (ENTQ - 1);
+    if (j == 0) {
+      const uint4* kp = reinterpret_cast<const uint4*>(key + i);
+      const uint4* ep = reinterpret_cast<const uint4*>(ent + i);
+#pragma unroll
+      for (uint32_t q = 0; q < ENTQ / 4; q++) {
+        const uint4 a = kp[q], b = ep[q];
+        col[64 * (4 * q + 0)] = a.x; col[64 * (4 * q + 1)] = a.y;
+        col[64 * (4 * q + 2)] = a.z; col[64 * (4 * q + 3)] = a.w;
+        col[64 * (ENTQ + 4 * q + 0)] = b.x; col[64 * (ENTQ + 4 * q + 1)] = b.y;
+        col[64 * (ENTQ + 4 * q + 2)] = b.z; col[64 * (ENTQ + 4 * q + 3)] = b.w;
+      }
+    }
+    g = col[64 * j];
+    en = col[64 * (ENTQ + j)];
+  }
+};
 
 // Thread t owns sorted entries [tK, tK+K).  One mixed add per entry (uniform
 // across the wave); at a bucket change the finished run is flushed:
@@ -332,8 +370,18 @@ __device__ __forceinline__ uint32_t chunk_len(uint32_t M, uint32_t T) { return M
 #endif
 template <class A>
 struct SegBases {
-  const A* p[MSM_MAXSEG];
+  const char* p[MSM_MAXSEG];
+  uint32_t stride;   // bytes between consecutive bases (packed or padded to 128-B lines)
 };
+// Base i of batch segment `seg` (the MSM owning the bucket).
+template <class A>
+ZK_DI const A* seg_base(const SegBases<A>& sb, uint32_t seg, uint32_t i) {
+  const char* b = sb.p[0];
+#pragma unroll
+  for (int k = 1; k < MSM_MAXSEG; k++)
+    if (seg == (uint32_t)k) b = sb.p[k];
+  return reinterpret_cast<const A*>(b + (size_t)i * sb.stride);
+}
 
 template <class C>
 __global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum(SegBases<typename C::A> sb, uint32_t segshift, uint32_t idx_mask,
@@ -352,9 +400,11 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum(SegBases<typena
   X acc;
   xyzz_set_inf(acc);
   uint32_t cur = key[start], run_start = start;
+  __shared__ uint32_t entq_lds[2 * ENTQ_LDS_WORDS];   // 128 threads = 2 waves
+  EntQ q(entq_lds);
   for (uint32_t e = start; e < end; e++) {
-    const uint32_t g = key[e];
-    const uint32_t en = ent[e];
+    uint32_t g, en;
+    q.next(key, ent, start, e, g, en);
     if (g != cur) {
       const bool head = (run_start == start) && (off[cur] < start);
       if (head) st_vec(&partials[2 * (size_t)t], acc);
@@ -364,12 +414,8 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum(SegBases<typena
       run_start = e;
     }
     if (en == MSM_DUMMY) continue;   // zero digit (shared-bucket plans)
-    const uint32_t seg = g >> segshift;   // batch: the MSM owning bucket g
-    const typename C::A* bases = sb.p[0];
-#pragma unroll
-    for (int k = 1; k < MSM_MAXSEG; k++)
-      if (seg == (uint32_t)k) bases = sb.p[k];
-    typename C::A a = ld_vec(&bases[en & idx_mask]);
+    // batch: bucket g >> segshift names the MSM whose bases entry en indexes
+    typename C::A a = ld_vec(seg_base(sb, g >> segshift, en & idx_mask));
     if (en & 0x80000000u) a.y = f_neg(a.y);
     if (!aff_is_inf(a)) acc = xyzz_madd(acc, a);
   }
@@ -411,9 +457,11 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(ZK_LAZ
   FlX acc;
   flx_set_inf(acc);
   uint32_t cur = key[start], run_start = start;
+  __shared__ uint32_t entq_lds[2 * ENTQ_LDS_WORDS];   // 128 threads = 2 waves
+  EntQ q(entq_lds);
   for (uint32_t e = start; e < end; e++) {
-    const uint32_t g = key[e];
-    const uint32_t en = ent[e];
+    uint32_t g, en;
+    q.next(key, ent, start, e, g, en);
     if (g != cur) {
       const bool head = (run_start == start) && (off[cur] < start);
       st_lazy(head ? &partials[2 * (size_t)t] : &buckets[cur], acc);
@@ -422,12 +470,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(ZK_LAZ
       run_start = e;
     }
     if (en == MSM_DUMMY) continue;
-    const uint32_t seg = g >> segshift;
-    const G1A* bases = sb.p[0];
-#pragma unroll
-    for (int k = 1; k < MSM_MAXSEG; k++)
-      if (seg == (uint32_t)k) bases = sb.p[k];
-    const G1A a = ld_vec(&bases[en & idx_mask]);
+    const G1A a = ld_vec(seg_base(sb, g >> segshift, en & idx_mask));
     if (aff_is_inf(a)) continue;
     FlA la{fl_from_fq(a.x), fl_from_fq(a.y)};
     if (en & 0x80000000u) la.y = fl_neg(la.y);
@@ -478,9 +521,11 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum_pair(SegBases<G
   XYZZ<Fq2h> acc;
   xyzz_set_inf(acc);
   uint32_t cur = key[start], run_start = start;
+  __shared__ uint32_t entq_lds[2 * ENTQ_LDS_WORDS];   // 128 threads = 2 waves
+  EntQ q(entq_lds);
   for (uint32_t e = start; e < end; e++) {
-    const uint32_t g = key[e];
-    const uint32_t en = ent[e];
+    uint32_t g, en;
+    q.next(key, ent, start, e, g, en);
     if (g != cur) {
       const bool head = (run_start == start) && (off[cur] < start);
       if (head) st_pair(&partials[2 * (size_t)t], acc);
@@ -490,12 +535,7 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum_pair(SegBases<G
       run_start = e;
     }
     if (en == MSM_DUMMY) continue;
-    const uint32_t seg = g >> segshift;
-    const G2A* bases = sb.p[0];
-#pragma unroll
-    for (int k = 1; k < MSM_MAXSEG; k++)
-      if (seg == (uint32_t)k) bases = sb.p[k];
-    const Fq* bp = reinterpret_cast<const Fq*>(&bases[en & idx_mask]) + h;
+    const Fq* bp = reinterpret_cast<const Fq*>(seg_base(sb, g >> segshift, en & idx_mask)) + h;
     Affine<Fq2h> a{{ld_vec(bp)}, {ld_vec(bp + 2)}};
     if (en & 0x80000000u) a.y = f_neg(a.y);
     if (!aff_is_inf(a)) acc = xyzz_madd(acc, a);
@@ -976,8 +1016,8 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
   const uint32_t n = p.n;   // all points of the batch (profiling units)
   const uint32_t nblk = ceil_div(p.G, MSM_SCAN_BLOCK);
   w.off.ensure(sizeof(uint32_t) * (p.G + 1));
-  w.ent.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
-  w.key.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
+  w.ent.ensure(sizeof(uint32_t) * (M + ENTQ));   // EntQ reads up to ENTQ - 1 past the end
+  w.key.ensure(sizeof(uint32_t) * (M + ENTQ));
   w.buckets.ensure(sizeof(X) * p.G);
   p.T = accum_threads<C>();
   p.fix_max = 8;
@@ -987,7 +1027,12 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
   w.rc.ensure(sizeof(X) * p.nrc);
   w.res.ensure(sizeof(X) * p.nq);
   SegBases<typename C::A> sb{};
-  for (int k = 0; k < nseg; k++) sb.p[k] = static_cast<const typename C::A*>(segs[k].bases);
+  sb.stride = segs[0].stride ? segs[0].stride : (uint32_t)sizeof(typename C::A);
+  for (int k = 0; k < nseg; k++) {
+    sb.p[k] = static_cast<const char*>(segs[k].bases);
+    if ((segs[k].stride ? segs[k].stride : (uint32_t)sizeof(typename C::A)) != sb.stride)
+      throw Error(ZK_ERR_ARG, "msm: batch segments with different base strides");
+  }
 
   Prof* pf = w.prof;
   const bool g2 = sizeof(typename C::A) == sizeof(G2A);
@@ -1144,18 +1189,18 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
 
 template <class C>
 void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scalars, int sw, uint32_t n,
-                int bits, hipStream_t st) {
+                int bits, hipStream_t st, uint32_t stride) {
   w.plan = msm_make_plan(n, bits, sw);
-  const MsmSeg seg{d_bases, d_scalars, n};
+  const MsmSeg seg{d_bases, d_scalars, n, stride};
   msm_launch_impl<C>(w, &seg, 1, sw, st);
 }
 
 template <class C>
 void msm_launch_shared(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scalars, int sw, uint32_t n,
-                       int bits, int c, hipStream_t st) {
+                       int bits, int c, hipStream_t st, uint32_t stride) {
   w.plan = msm_make_plan_shared(n, bits, sw, c);
   if ((uint64_t)n * w.plan.nwin >= MSM_DUMMY) throw Error(ZK_ERR_ARG, "msm: too many window bases");
-  const MsmSeg seg{d_bases, d_scalars, n};
+  const MsmSeg seg{d_bases, d_scalars, n, stride};
   msm_launch_impl<C>(w, &seg, 1, sw, st);
 }
 
@@ -1241,6 +1286,40 @@ void msm_precompute_windows(typename C::A* d_bases, size_t n, int W, int c, hipS
     batch_normalize<C>(xs.as<typename C::X>(), n, pre.as<typename C::F>(), d_bases + (size_t)w * n, st);
   }
   ZK_HIP(hipStreamSynchronize(st));   // xs / pre die here
+}
+
+// out element i (ow 16-B words) = in element i (iw words) followed by zeros
+__global__ void __launch_bounds__(256) k_pad_copy(const uint4* __restrict__ in, size_t n, uint32_t iw, uint32_t ow,
+                                                  uint4* __restrict__ out) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * ow) return;
+  const size_t i = t / ow;
+  const uint32_t k = (uint32_t)(t - i * ow);
+  out[t] = k < iw ? in[i * iw + k] : make_uint4(0, 0, 0, 0);
+}
+
+static bool base_pad_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("ZK_BASE_PAD");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
+template <class C>
+uint32_t msm_pad_bases(DevBuf& d, size_t n, hipStream_t st) {
+  constexpr uint32_t sz = sizeof(typename C::A), padded = (sz + 127) / 128 * 128;
+  if (!base_pad_enabled() || padded == sz) return 0;
+  DevBuf out;
+  out.ensure((size_t)padded * std::max<size_t>(n, 1));
+  if (n) {
+    k_pad_copy<<<ceil_div(n * (padded / 16), 256), 256, 0, st>>>(d.as<uint4>(), n, sz / 16, padded / 16,
+                                                                  out.as<uint4>());
+    ZK_LAUNCH_CHECK();
+  }
+  ZK_HIP(hipStreamSynchronize(st));   // the packed copy dies here
+  d = std::move(out);
+  return padded;
 }
 
 template <class C>
@@ -1375,9 +1454,11 @@ void host_to_abi<G2>(const host::X<host::Fq2>& p, uint64_t* w) {
 }
 
 #define ZK_MSM_INST(C)                                                                               \
-  template void msm_launch<C>(MsmWork&, const C::A*, const uint64_t*, int, uint32_t, int, hipStream_t); \
+  template void msm_launch<C>(MsmWork&, const C::A*, const uint64_t*, int, uint32_t, int, hipStream_t,  \
+                              uint32_t);                                                              \
   template void msm_launch_shared<C>(MsmWork&, const C::A*, const uint64_t*, int, uint32_t, int, int,   \
-                                     hipStream_t);                                                    \
+                                     hipStream_t, uint32_t);                                          \
+  template uint32_t msm_pad_bases<C>(DevBuf&, size_t, hipStream_t);                                  \
   template void msm_precompute_windows<C>(C::A*, size_t, int, int, hipStream_t);                       \
   template void batch_normalize<C>(const C::X*, size_t, C::F*, C::A*, hipStream_t);                    \
   template void msm_download<C>(MsmWork&, hipStream_t);                                              \

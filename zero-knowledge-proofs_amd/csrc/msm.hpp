@@ -77,6 +77,7 @@ struct MsmSeg {
   const void* bases;
   const uint64_t* scalars;
   uint32_t n;
+  uint32_t stride = 0;   // bytes between bases (0 = sizeof the affine point)
 };
 
 MsmPlan msm_make_plan(uint32_t n, int bits, int sw, int force_c = 0);
@@ -103,11 +104,11 @@ struct MsmWork {
 // n scalars of `sw` u64 words each (canonical little-endian, < 2^bits).
 template <class C>
 void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scalars, int sw,
-                uint32_t n, int bits, hipStream_t st);
+                uint32_t n, int bits, hipStream_t st, uint32_t stride = 0);
 // Same over window-shifted bases: d_bases holds nwin x n points, window-major.
 template <class C>
 void msm_launch_shared(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scalars, int sw,
-                       uint32_t n, int bits, int c, hipStream_t st);
+                       uint32_t n, int bits, int c, hipStream_t st, uint32_t stride = 0);
 // Up to MSM_MAXSEG independent MSMs over window-shifted bases with 64-bit
 // scalars, run as ONE key pass / sort / accumulate / merge / bucket
 // reduction: MSM k owns buckets [k 2^s, (k+1) 2^s).  The latency-bound
@@ -119,6 +120,13 @@ void msm_launch_batch(MsmWork& w, const MsmSeg* segs, int nseg, int bits, int c,
 // capacity W n).  One-time, at proving-key upload.
 template <class C>
 void msm_precompute_windows(typename C::A* d_bases, size_t n, int W, int c, hipStream_t st);
+// Base gathers by the accumulate are random: a packed 96-B G1 point straddles
+// two 128-B lines half the time (192-B G2: always 2-3 lines).  Padding each
+// point to whole lines (G1 128 B, G2 256 B) makes every gather exactly one
+// (two) line(s).  Returns the new stride in bytes, or 0 (packed) when
+// ZK_BASE_PAD=0; `d` is replaced by the padded copy of its n points.
+template <class C>
+uint32_t msm_pad_bases(DevBuf& d, size_t n, hipStream_t st);
 // XYZZ -> affine for n points with one Fermat inversion per 16-point chunk
 // (pre: n field elements of scratch).
 template <class C>

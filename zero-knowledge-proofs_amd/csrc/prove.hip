@@ -312,6 +312,8 @@ void pk_precompute_windows(zk_ctx* ctx, zk_pk_dev& pk) {
     if (slot == MSM_B2) msm_precompute_windows<G2>(big.as<G2A>(), n, PROVE_WIN, PROVE_WIN_C, st);
     else msm_precompute_windows<G1>(big.as<G1A>(), n, PROVE_WIN, PROVE_WIN_C, st);
     ZK_HIP(hipStreamSynchronize(st));
+    pk.stride[slot] = slot == MSM_B2 ? msm_pad_bases<G2>(big, n * PROVE_WIN, st)
+                                     : msm_pad_bases<G1>(big, n * PROVE_WIN, st);
     pk.bases[slot] = std::move(big);
   }
   pk.win = PROVE_WIN;
@@ -469,16 +471,18 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
     if (slot == MSM_B2) {
       if (pk->win > 1)
         msm_launch_shared<G2>(ctx->msm[slot], pk->bases[slot].as<G2A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64,
-                              pk->win_c, ss);
+                              pk->win_c, ss, pk->stride[slot]);
       else
-        msm_launch<G2>(ctx->msm[slot], pk->bases[slot].as<G2A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64, ss);
+        msm_launch<G2>(ctx->msm[slot], pk->bases[slot].as<G2A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64, ss,
+                       pk->stride[slot]);
       msm_download<G2>(ctx->msm[slot], ss);
     } else {
       if (pk->win > 1)
         msm_launch_shared<G1>(ctx->msm[slot], pk->bases[slot].as<G1A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64,
-                              pk->win_c, ss);
+                              pk->win_c, ss, pk->stride[slot]);
       else
-        msm_launch<G1>(ctx->msm[slot], pk->bases[slot].as<G1A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64, ss);
+        msm_launch<G1>(ctx->msm[slot], pk->bases[slot].as<G1A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64, ss,
+                       pk->stride[slot]);
       msm_download<G1>(ctx->msm[slot], ss);
     }
   };
@@ -522,7 +526,8 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       for (size_t k = 0; k < grp.size(); k++) {
         const int slot = grp[k];
         prep_scalars(slot, gs);
-        segs[k] = MsmSeg{pk->bases[slot].p, ctx->scal[slot].as<uint64_t>(), pk->count[slot] + pk->extras[slot]};
+        segs[k] = MsmSeg{pk->bases[slot].p, ctx->scal[slot].as<uint64_t>(), pk->count[slot] + pk->extras[slot],
+                         pk->stride[slot]};
       }
       MsmWork& w = ctx->msm[grp[0]];
       if (sched == 3) {

@@ -91,8 +91,17 @@ def phase_table(prof):
 # Peak: tools/mulbench.hip, best radix-2^28 variant, 72.2 G Fq-mul/s x 392 =
 # 28.3 T v_mad_u64_u32/s.
 MADS_PER_MADD = 8 * 196 + 2 * 105 + 9 * 196
-PROVE_WINDOWS = 4
 VALU_PEAK_TMADS = 28.3
+
+
+def prove_windows(constraints_per_shard):
+    """Digit windows of the prove MSMs' 64-bit scalars: the library's rule
+    (prove.hip prove_win_c) -- c = 16 (4 windows), c = 22 (3 windows) from
+    2^24 constraints per key shard; ZK_PROVE_WIN_C overrides."""
+    c = int(os.environ.get("ZK_PROVE_WIN_C", "0") or 0)
+    if not 8 <= c <= 22:
+        c = 22 if constraints_per_shard >= 1 << 24 else 16
+    return -(-64 // c)
 
 
 def traffic_for(log_n):
@@ -127,7 +136,7 @@ def roofline_from(prof, log_n, overlapped=None):
     algo_bytes = G1_PAIR_BYTES * units
     achieved = algo_bytes / (ms / 1e3) / 1e9
     traffic, tsrc = traffic_for(log_n)
-    tmads = units * PROVE_WINDOWS * MADS_PER_MADD / (ms / 1e3) / 1e12
+    tmads = units * prove_windows(1 << log_n) * MADS_PER_MADD / (ms / 1e3) / 1e12
     out = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
            "traffic_source": tsrc, "kernel": "k_msm_accum<G1>",

@@ -1007,7 +1007,8 @@ template <class C>
 static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hipStream_t st) {
   using X = typename C::X;
   MsmPlan& p = w.plan;
-  if (p.G > (uint32_t)MSM_SCAN_BLOCK * 1024) throw Error(ZK_ERR_ARG, "msm: too many buckets");
+  if (p.G > (uint32_t)MSM_SCAN_BLOCK * 1024 && !(msm_sort_mode() == 0 || p.shared))
+    throw Error(ZK_ERR_ARG, "msm: too many buckets for the counting sort");
   if (nseg < 1 || nseg > MSM_MAXSEG || (nseg > 1 && (!p.shared || sw != 1)))
     throw Error(ZK_ERR_ARG, "msm: bad batch");
   size_t M = 0;

@@ -342,25 +342,22 @@ static int ntt_device(zk_ctx* ctx, void* d_data, uint32_t log_n, int dir, const 
   auto to_dev = [](const host::Fr& h) { Fr x; const host::Fr v = host::fr_to_dev(h); std::memcpy(x.v, v.l, 32); return x; };
   const host::Fr one = host::fr_one();
   const host::Fr ninv = host::fr_inv(host::fr_from_u64(n));
+  // natural -> natural (ntt_natural: the bit reversal is the first pass's gather)
   if (dir > 0) {
     const Fr* ltab = nullptr;
     if (coset) {                                   // a_i *= g^i, fused into the first pass's load
       fr_powers(b, to_dev(host::fr_to_mont(coset->l)), to_dev(one), n, st);
       ltab = b;
     }
-    ntt_dif(a, dom, false, st, &ctx->prof, d, ltab);   // natural d -> bit-reversed a
-    fr_bitrev_scale(a, d, log_n, nullptr, nullptr, st);
+    ntt_natural(d, d, a, dom, false, st, &ctx->prof, ltab, nullptr, nullptr);
+  } else if (coset) {                              // out_i *= n^-1 g^-i, fused into the last pass's store
+    host::Fr g = host::fr_to_mont(coset->l);
+    if (host::fr_is_zero(g)) return ZK_ERR_ARG;
+    fr_powers(b, to_dev(host::fr_inv(g)), to_dev(ninv), n, st);
+    ntt_natural(d, d, a, dom, true, st, &ctx->prof, nullptr, b, nullptr);
   } else {
-    ntt_dif(a, dom, true, st, &ctx->prof, d, nullptr);
-    if (coset) {                                   // out_i *= n^-1 g^-i
-      host::Fr g = host::fr_to_mont(coset->l);
-      if (host::fr_is_zero(g)) return ZK_ERR_ARG;
-      fr_powers(b, to_dev(host::fr_inv(g)), to_dev(ninv), n, st);
-      fr_bitrev_scale(a, d, log_n, b, nullptr, st);
-    } else {
-      const Fr c = to_dev(ninv);
-      fr_bitrev_scale(a, d, log_n, nullptr, &c, st);
-    }
+    const Fr c = to_dev(ninv);
+    ntt_natural(d, d, a, dom, true, st, &ctx->prof, nullptr, nullptr, &c);
   }
   return ZK_OK;
 }

@@ -112,6 +112,23 @@ __device__ __forceinline__ void ntt_rounds(Fr* sh, const Fr* __restrict__ sm, ui
   }
 }
 
+// Where a pass reads and writes.  Default: in place on `dst`.  IO_GATHER
+// (first DIT pass only: s_lo = 0, one column per tile) reads element p of
+// the pass from src[bitrev(p)] -- natural-order input of a DIT transform,
+// so no separate permutation pass -- and orders its tiles so that the 4
+// tiles whose gathers share 128-byte lines run back to back on one XCD.
+// ltab: factor on load (indexed like the source); stab / scale: factor on
+// store (indexed like the destination).
+constexpr uint32_t IO_GATHER = 1, IO_SCALE = 2;
+struct PassIO {
+  const Fr* src;
+  Fr* dst;
+  const Fr* ltab;
+  const Fr* stab;
+  Fr scale;
+  uint32_t flags;
+};
+
 // One pass = one four-step level.  The block of N = 2^(s_lo+ns) elements
 // at hi is a 2^ns x 2^s_lo matrix (row r, column lo); the pass runs the
 // 2^ns-point sub-transform down every column of its tile (C columns), whose
@@ -122,9 +139,8 @@ __device__ __forceinline__ void ntt_rounds(Fr* sh, const Fr* __restrict__ sm, ui
 // sum_a x[a n2 + b] w_n1^(a k1); sub-transforms in place leave element k at
 // bitrev(k1) n2 + bitrev(k2) = bitrev_(log n)(k): exactly radix-2 DIF order.
 template <bool DIT>
-__global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(Fr* __restrict__ data, const Fr* src, const Fr* ltab,
-                                                          NttTabs tabs, uint32_t log_n, uint32_t s_lo, uint32_t ns,
-                                                          uint32_t logC) {
+__global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(PassIO io, NttTabs tabs, uint32_t log_n, uint32_t s_lo,
+                                                          uint32_t ns, uint32_t logC) {
   extern __shared__ uint4 sh_raw[];
   Fr* sh = reinterpret_cast<Fr*>(sh_raw);
   const uint32_t C = 1u << logC;
@@ -135,19 +151,20 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(Fr* __restrict__ data,
   // blocks (which share 128-byte lines when tiles are 1-2 columns wide) meet
   // in one XCD's L2
   const uint32_t G = gridDim.x;
-  const uint32_t tile = (G & 7) ? blockIdx.x : (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  uint32_t tile = (G & 7) ? blockIdx.x : (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  const bool gather = io.flags & IO_GATHER;
+  if (gather && log_n > ns) tile = bitrev32(tile, log_n - ns);   // gathers of neighbouring tiles share lines
   const uint32_t hi = tile / lo_blocks;
   const uint32_t lo0 = (tile % lo_blocks) << logC;
   const size_t base = ((size_t)hi << (s_lo + ns)) + lo0;
   const uint32_t tw_shift = log_n - s_lo - ns;          // omega_N = omega_n^(2^tw_shift)
 
-  // src: the first pass of an out-of-place transform reads another buffer;
-  // ltab: an elementwise factor on load (a coset's g^i, natural order)
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) {
     const uint32_t r = k >> logC, c = k & (C - 1);
     const size_t gi = base + ((size_t)r << s_lo) + c;
-    Fr v = ld_vec(&src[gi]);
-    if (ltab) v = fp_mul(v, ld_vec(&ltab[gi]));
+    const size_t si = gather ? bitrev32((uint32_t)gi, log_n) : gi;
+    Fr v = ld_vec(&io.src[si]);
+    if (io.ltab) v = fp_mul(v, ld_vec(&io.ltab[si]));
     if (DIT && s_lo) v = fp_mul(v, tw_full(tabs, ((lo0 + c) * bitrev32(r, ns)) << tw_shift, log_n));
     st_vec(&sh[k], v);
   }
@@ -155,32 +172,42 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(Fr* __restrict__ data,
   ntt_rounds<DIT>(sh, tabs.sm, ns, logC);
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) {
     const uint32_t r = k >> logC, c = k & (C - 1);
+    const size_t go = base + ((size_t)r << s_lo) + c;
     Fr v = ld_vec(&sh[k]);
     if (!DIT && s_lo) v = fp_mul(v, tw_full(tabs, ((lo0 + c) * bitrev32(r, ns)) << tw_shift, log_n));
-    st_vec(&data[base + ((size_t)r << s_lo) + c], v);
+    if (io.stab) v = fp_mul(v, ld_vec(&io.stab[go]));
+    else if (io.flags & IO_SCALE) v = fp_mul(v, io.scale);
+    st_vec(&io.dst[go], v);
   }
 }
 
-static void run_pass(bool dit, Fr* d, const NttTabs& t, uint32_t log_n, uint32_t s_lo, uint32_t ns,
-                     hipStream_t st, const Fr* src = nullptr, const Fr* ltab = nullptr) {
+static void run_pass_io(bool dit, const PassIO& io, const NttTabs& t, uint32_t log_n, uint32_t s_lo, uint32_t ns,
+                        hipStream_t st) {
   const uint32_t logC = std::min<uint32_t>(s_lo, NTT_TILE_LOG - ns);
   const uint32_t tiles = (uint32_t)((1ull << log_n) >> (ns + logC));
   const size_t lds = sizeof(Fr) << (ns + logC);
   if (dit)
-    k_ntt_pass<true><<<tiles, NTT_THREADS, lds, st>>>(d, src ? src : d, ltab, t, log_n, s_lo, ns, logC);
+    k_ntt_pass<true><<<tiles, NTT_THREADS, lds, st>>>(io, t, log_n, s_lo, ns, logC);
   else
-    k_ntt_pass<false><<<tiles, NTT_THREADS, lds, st>>>(d, src ? src : d, ltab, t, log_n, s_lo, ns, logC);
+    k_ntt_pass<false><<<tiles, NTT_THREADS, lds, st>>>(io, t, log_n, s_lo, ns, logC);
   ZK_LAUNCH_CHECK();
+}
+
+static void run_pass(bool dit, Fr* d, const NttTabs& t, uint32_t log_n, uint32_t s_lo, uint32_t ns,
+                     hipStream_t st, const Fr* src = nullptr, const Fr* ltab = nullptr) {
+  run_pass_io(dit, PassIO{src ? src : d, d, ltab, nullptr, Fr{}, 0u}, t, log_n, s_lo, ns, st);
 }
 
 // Pass plan, top (first DIF pass) to bottom: the contiguous pass (s_lo = 0)
 // takes up to 11 stages; the rest are split evenly into strided passes of
-// <= ZK_NTT_MAXSTRIDED stages (default 9: tiles keep >= 4 consecutive
-// columns, 128-byte rows).
+// <= ZK_NTT_MAXSTRIDED stages (default 11: at 2^22 two passes instead of
+// three, 0.580 vs 0.609 ms with depth 9, profiles/r02_ntt_sweep.txt; a
+// one-column tile's 32-byte rows share lines with its neighbours, which the
+// XCD-aware tile order keeps in one L2).
 static uint32_t max_strided() {
   static const uint32_t v = [] {
     const char* e = getenv("ZK_NTT_MAXSTRIDED");
-    return e ? (uint32_t)std::max(1, std::min(NTT_TILE_LOG, atoi(e))) : (uint32_t)(NTT_TILE_LOG - 2);
+    return e ? (uint32_t)std::max(1, std::min(NTT_TILE_LOG, atoi(e))) : (uint32_t)NTT_TILE_LOG;
   }();
   return v;
 }
@@ -223,6 +250,41 @@ void ntt_dit(Fr* d, const NttDomain& dom, bool inv, hipStream_t st, Prof* pf) {
   for (auto it = plan.rbegin(); it != plan.rend(); ++it) {
     run_pass(true, d, t, L, s_lo, *it, st);
     s_lo += *it;
+  }
+  if (pf) pf->end(st, ph);
+}
+
+// Natural order in and out (the reference's fft / ifft): DIT passes, the
+// first gathering its tiles from the bit-reversed positions of src (times
+// ltab[i] when given), the last writing dst (times stab[i] or *scale).  No
+// standalone permutation pass: at 2^22, 2 HBM round trips instead of 3
+// passes plus a bit reversal.  With more than one pass the intermediate
+// levels live in tmp (n elements), so src may equal dst.
+void ntt_natural(Fr* dst, const Fr* src, Fr* tmp, const NttDomain& dom, bool inv, hipStream_t st, Prof* pf,
+                 const Fr* ltab, const Fr* stab, const Fr* scale) {
+  const uint32_t L = dom.log_n;
+  if (L == 0) return;
+  const int ph = pf ? pf->begin(st, "ntt", (uint64_t)1 << L) : -1;
+  const NttTabs t = tabs_of(dom, inv);
+  const std::vector<uint32_t> plan = pass_plan(L);
+  const size_t P = plan.size();
+  uint32_t s_lo = 0;
+  for (size_t i = 0; i < P; i++) {
+    const uint32_t ns = plan[P - 1 - i];
+    PassIO io{i == 0 ? src : tmp, i + 1 == P ? dst : tmp, nullptr, nullptr, Fr{}, 0u};
+    if (i == 0) {
+      io.flags |= IO_GATHER;
+      io.ltab = ltab;
+    }
+    if (i + 1 == P) {
+      io.stab = stab;
+      if (scale) {
+        io.scale = *scale;
+        io.flags |= IO_SCALE;
+      }
+    }
+    run_pass_io(true, io, t, L, s_lo, ns, st);
+    s_lo += ns;
   }
   if (pf) pf->end(st, ph);
 }

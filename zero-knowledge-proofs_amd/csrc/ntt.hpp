@@ -67,6 +67,12 @@ inline NttTabs tabs_of(const NttDomain& dom, bool inv) {
 void ntt_dif(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st, Prof* pf = nullptr,
              const Fr* src = nullptr, const Fr* ltab = nullptr);
 void ntt_dit(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st, Prof* pf = nullptr);
+// Natural order in (src) and out (dst), the API transform: DIT passes whose
+// first pass gathers from bit-reversed positions; ltab: factor on the input
+// (natural index), stab / scale: factor on the output.  tmp: n elements of
+// scratch (src may equal dst).
+void ntt_natural(Fr* dst, const Fr* src, Fr* tmp, const NttDomain& dom, bool inverse_twiddles, hipStream_t st,
+                 Prof* pf, const Fr* ltab, const Fr* stab, const Fr* scale);
 
 // d <- NTT(tab[bitrev(i)] * iNTT(d)) with the inverse DIF's last pass, the
 // scale and the forward DIT's first pass fused into one tile kernel (the

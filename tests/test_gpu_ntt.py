@@ -45,8 +45,9 @@ def test_ntt_coset_roundtrip(ctx, oracle):
     assert np.array_equal(ctx.ntt(y, inverse=True, coset=7), x)
 
 
-@pytest.mark.parametrize("log_n", [20, 22])
+@pytest.mark.parametrize("log_n", [20, 22, 23])
 def test_ntt_roundtrip_large(ctx, oracle, log_n):
+    """2^23: three DIT passes (11 gathered + 6 + 6 stages) on the natural-order path."""
     x = oracle.random_fr(1 << log_n, 7)
     y = ctx.ntt(x)
     assert np.array_equal(ctx.ntt(y, inverse=True), x)

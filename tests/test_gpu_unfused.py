@@ -33,3 +33,28 @@ def test_lazy_accumulate_matches_oracle():
                           "16"], env=env, capture_output=True, text=True, timeout=280)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
     assert res.stdout.count(" ok") == 3
+
+
+@pytest.mark.timeout(300)
+def test_packed_bases_match_oracle():
+    """ZK_BASE_PAD=0: the proving key's window copies stay packed (96-byte G1,
+    192-byte G2 points) instead of line-padded -- the accumulate's base
+    stride is a launch parameter, so both layouts must prove the same bytes."""
+    env = dict(os.environ, ZK_BASE_PAD="0")
+    res = subprocess.run([sys.executable, os.path.join(HERE, "unfused_quotient_check.py"), "ZK_BASE_PAD=0", "3", "10",
+                          "14"], env=env, capture_output=True, text=True, timeout=280)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
+    assert res.stdout.count(" ok") == 3
+
+
+@pytest.mark.timeout(300)
+def test_three_window_plan_matches_oracle():
+    """ZK_PROVE_WIN_C=22: the 3-window / 2^21-bucket plan the library picks
+    from 2^24 constraints up, forced at small sizes (the batch keys reach
+    23 bits, so the radix sort, merge and bucket reduction see 2^21-bucket
+    segments)."""
+    env = dict(os.environ, ZK_PROVE_WIN_C="22")
+    res = subprocess.run([sys.executable, os.path.join(HERE, "unfused_quotient_check.py"), "ZK_PROVE_WIN_C=22", "4",
+                          "12"], env=env, capture_output=True, text=True, timeout=280)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
+    assert res.stdout.count(" ok") == 2

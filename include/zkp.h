@@ -151,11 +151,12 @@ int zk_msm_g2(zk_ctx *ctx, const zk_g2_affine *bases, size_t nbases,
 typedef struct zk_msm_bases zk_msm_bases;
 int zk_msm_g1_upload(zk_ctx *ctx, const zk_g1_affine *bases, size_t n, zk_msm_bases **out);
 int zk_msm_g2_upload(zk_ctx *ctx, const zk_g2_affine *bases, size_t n, zk_msm_bases **out);
-/* Same, plus ceil(scalar_bits / 16) window-shifted copies 2^(16 w) P of every
- * base (scalar_bits = 0 -> 255): later zk_msm_*_dev calls with scalars of at
- * most scalar_bits bits sum every digit window into ONE bucket set (one
- * bucket reduction, no per-window Horner).  Costs ceil(scalar_bits/16) x the
- * base memory and a one-time precomputation.  No reference counterpart
+/* Same, plus ceil(scalar_bits / c) window-shifted copies 2^(c w) P of every
+ * base (c = 16 up to 64-bit scalars, else 20; scalar_bits = 0 -> 255):
+ * later zk_msm_*_dev calls with scalars of at most scalar_bits bits sum every
+ * digit window into ONE bucket set (one bucket reduction, no per-window
+ * Horner).  Costs ceil(scalar_bits / c) x the base memory (points padded to
+ * whole 128-byte lines) and a one-time precomputation.  No reference counterpart
  * (fixed-base preprocessing of bases reused across MSMs, as in the prover). */
 int zk_msm_g1_upload_windows(zk_ctx *ctx, const zk_g1_affine *bases, size_t n, uint32_t scalar_bits,
                              zk_msm_bases **out);

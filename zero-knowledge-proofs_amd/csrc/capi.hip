@@ -207,10 +207,23 @@ int zk_msm_g2(zk_ctx* ctx, const zk_g2_affine* bases, size_t nb, const zk_fr* sc
 }
 
 // Window-shifted uploads (zk_msm_*_upload_windows): c = 16-bit digit windows,
-// W = ceil(scalar_bits / 16) copies 2^(16 w) P of every base, so every
+// W = ceil(scalar_bits / c) copies 2^(c w) P of every base, so every
 // later MSM of <= scalar_bits-bit scalars sums all its windows into ONE
 // bucket set (msm_launch_shared; the prove path's trick, prove.hip).
-constexpr int MSM_UPLOAD_WIN_C = 16;
+// Window width c: 16 up to 64-bit scalars (4 windows, 2^15 buckets), 20 for
+// wider ones -- 13 windows over 2^19 buckets instead of 16 over 2^15: the
+// 2^20 full-width MSM 3.79-3.87 vs 3.92-4.01 ms; c = 18, 19, 22 lose
+// (4.5-5.0 ms; profiles/r02_upload_win_sweep.txt).  ZK_UPLOAD_WIN_C
+// overrides (8..22).
+static int upload_win_c(uint32_t win_bits) {
+  static const int env = [] {
+    const char* e = getenv("ZK_UPLOAD_WIN_C");
+    const int v = e ? atoi(e) : 0;
+    return v >= 8 && v <= 22 ? v : 0;
+  }();
+  if (env) return env;
+  return win_bits > 64 ? 20 : 16;
+}
 
 template <class C, class ABI>
 static int msm_upload(zk_ctx* ctx, const ABI* bases, size_t n, int group, uint32_t win_bits, zk_msm_bases** out) {
@@ -221,6 +234,7 @@ static int msm_upload(zk_ctx* ctx, const ABI* bases, size_t n, int group, uint32
     b->device = ctx->device;
     b->group = group;
     b->n = n;
+    const int MSM_UPLOAD_WIN_C = upload_win_c(win_bits);
     const int W = win_bits ? (int)((win_bits + MSM_UPLOAD_WIN_C - 1) / MSM_UPLOAD_WIN_C) : 1;
     if ((uint64_t)n * W >= 0x7fffffffull) throw Error(ZK_ERR_ARG, "msm: too many window bases");
     b->bases.ensure(sizeof(typename C::A) * std::max<size_t>(n * W, 1));

@@ -246,21 +246,25 @@ def msm_g1_bench(zkp, ctx, log_n, steps, warmup, seed):
     bases = crs.pk.h_g1
     sc = random_fr(np.random.default_rng(seed + 7), n)
     d_sc = torch.from_numpy(sc.view(np.int64)).to(f"cuda:{ctx.device}")
+    sc64 = np.zeros_like(sc)                 # also the prove path's 64-bit scalars
+    sc64[:, 0] = sc[:, 0]
+    d_sc64 = torch.from_numpy(sc64.view(np.int64)).to(f"cuda:{ctx.device}")
 
-    def measure(windows):
-        """windows: bases uploaded with their window-shifted copies (13 at c = 20 for 255-bit scalars)
-        (zk_msm_g1_upload_windows: one bucket set), else plain."""
+    def measure(windows, bits=255):
+        """windows: bases uploaded with their window-shifted copies (13 at c = 20 for 255-bit scalars,
+        4 at c = 16 for 64-bit ones; zk_msm_g1_upload_windows: one bucket set), else plain."""
         hb = C.c_void_p()
         up = zkp.lib().zk_msm_g1_upload_windows if windows else zkp.lib().zk_msm_g1_upload
-        args = (C.c_void_p(ctx._h), zkp._p(bases), C.c_size_t(n)) + ((C.c_uint32(255),) if windows else ())
+        args = (C.c_void_p(ctx._h), zkp._p(bases), C.c_size_t(n)) + ((C.c_uint32(bits),) if windows else ())
         t_up = time.perf_counter()
         zkp._check(up(*args, C.byref(hb)), ctx, "upload")
         t_up = time.perf_counter() - t_up
         out = np.zeros(13, dtype=np.uint64)
+        d = d_sc if bits > 64 else d_sc64
 
         def run():
-            zkp._check(zkp.lib().zk_msm_g1_dev(C.c_void_p(ctx._h), hb, C.c_void_p(d_sc.data_ptr()), C.c_size_t(n),
-                                                C.c_uint32(255), zkp._p(out)), ctx, "zk_msm_g1_dev")
+            zkp._check(zkp.lib().zk_msm_g1_dev(C.c_void_p(ctx._h), hb, C.c_void_p(d.data_ptr()), C.c_size_t(n),
+                                                C.c_uint32(bits), zkp._p(out)), ctx, "zk_msm_g1_dev")
         for _ in range(warmup):
             run()
         torch.cuda.synchronize()
@@ -276,10 +280,18 @@ def msm_g1_bench(zkp, ctx, log_n, steps, warmup, seed):
     dt_plain, _, r2 = measure(False)
     if not np.array_equal(r1, r2):
         raise SystemExit("windowed and plain MSM disagree")
+    dt64, _, r3 = measure(True, 64)
+    dt64_plain, _, r4 = measure(False, 64)
+    if not np.array_equal(r3, r4):
+        raise SystemExit("windowed and plain 64-bit MSM disagree")
     return {"pairs_per_s": round(n / dt, 1), "n": n, "scalar_bits": 255, "ms_per_msm": round(dt * 1e3, 3),
             "bases": "uploaded once with 13 window-shifted copies (c = 20; zk_msm_g1_upload_windows, %.0f ms)" % (t_up * 1e3),
             "plain": {"pairs_per_s": round(n / dt_plain, 1), "ms_per_msm": round(dt_plain * 1e3, 3),
                       "bases": "uploaded once, one copy (zk_msm_g1_upload)"},
+            "bits64": {"pairs_per_s": round(n / dt64, 1), "ms_per_msm": round(dt64 * 1e3, 3),
+                       "plain_ms_per_msm": round(dt64_plain * 1e3, 3),
+                       "note": "the same bases with the low 64 bits of the scalars (the prove path's lo64 "
+                               "distribution): 4 window copies at c = 16; checked equal to the plain upload"},
             "parity": "tests/test_gpu_headline.py::test_msm_g1_2p20_closed_form (same sizes, closed form)"}
 
 
@@ -297,11 +309,11 @@ def ntt_bench(zkp, ctx, log_n, steps, warmup, seed):
     def run(direction):
         zkp._check(L.zk_ntt_fr_dev(h, C.c_void_p(d.data_ptr()), C.c_uint32(log_n), C.c_int(direction), None),
                    ctx, "zk_ntt_fr_dev")
-    for _ in range(warmup):
+    for _ in range(max(warmup, 10)):   # ~12 ms of warmup: the clocks ramp up
         run(1)
         run(-1)
     torch.cuda.synchronize()
-    steps = max(steps, 10)
+    steps = max(steps, 20)
     t0 = time.perf_counter()
     for _ in range(steps):
         run(1)
@@ -385,6 +397,12 @@ def main():
         n = (1 << args.log_n) * world
     log_n_total = n.bit_length() - 1
     params, r, s = setup_params(args.seed)
+    extra = {}
+    if world == 1 and not args.no_msm:
+        # configs[2] first, on a fresh context (after the prove's multi-GB key
+        # allocations the same transform measured ~20 % slower)
+        log("[bench] NTT 2^22 (configs[2])")
+        extra["ntt"] = ntt_bench(zkp, ctx, 22, args.steps, args.warmup, args.seed + 31)
     log(f"[bench] setup 2^{log_n_total}-constraint synthetic circuit on GPU (shard {rank}/{world})")
     qap = zkp.QAP(zkp.CSRMatrices.synthetic(n))
     t0 = time.perf_counter()
@@ -426,7 +444,6 @@ def main():
     value = n / (elapsed / args.steps)
     g1_pairs, g2_pairs = prove_msm_pairs(n)
 
-    extra = {}
     roofline = None
     if rank == 0 and world == 1:
         # the dominant kernel's own duration: the same proves, every kernel in
@@ -470,8 +487,6 @@ def main():
         if not args.no_msm:
             log("[bench] G1 MSM 2^20 (configs[1])")
             extra["msm_g1"] = msm_g1_bench(zkp, ctx, 20, args.steps, args.warmup, args.seed + 11)
-            log("[bench] NTT 2^22 (configs[2])")
-            extra["ntt"] = ntt_bench(zkp, ctx, 22, args.steps, args.warmup, args.seed + 31)
         if not args.no_cpu_baseline:
             log(f"[bench] CPU baseline: oracle prove at 2^{log_n_total} on all cores, 2^{args.cpu_log_n} on 1 thread")
             extra["cpu_baseline"] = cpu_baseline(zkp, ctx, n, params, r, s, z_host, proof, args.cpu_log_n,

@@ -18,6 +18,10 @@ def test_constants(oracle, pyref):
     assert pow(w, 1 << 32, R) == 1 and pow(w, 1 << 31, R) != 1
     # omega_2^20 as tabulated in SURVEY.md 8(a)-a5
     assert oracle.fr_root_of_unity(20) == 0x03E1C54BCB947035A57A6E07CB98DE4A2F69E02D265E09D9FECE7E0E39898D4B
+    # ... and at the other config sizes (2^21 the reference FFT at configs[3], 2^22 configs[2], 2^24 configs[4])
+    assert oracle.fr_root_of_unity(21) == 0x47C8B5817018AF4FC70D0874B0691D4E46B3105F04DB5844CD3979122D3EA03A
+    assert oracle.fr_root_of_unity(22) == 0x0ABE6A5E5ABCAA32F2D38F10FBB8D1BBE08FEC7C86389BEEC6E7A6FFB08E3363
+    assert oracle.fr_root_of_unity(24) == 0x291CF6D68823E6876E0BCD91EE76273072CF6A8029B7D7BC92CF4DEB77BD779C
     g1, g2 = oracle.g1_generator(), oracle.g2_generator()
     assert oracle.g1_on_curve(g1) and oracle.g2_on_curve(g2)
     assert oracle.g1_mul(g1, R)[12] == 1 and oracle.g2_mul(g2, R)[24] == 1     # r * G = O

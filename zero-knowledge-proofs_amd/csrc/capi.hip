@@ -64,6 +64,7 @@ zk_ctx* zk_ctx_create(int device) {
     ZK_HIP(hipEventCreateWithFlags(&c->ev_scal, hipEventDisableTiming));
     ZK_HIP(hipEventCreateWithFlags(&c->ev_hsort, hipEventDisableTiming));
     for (auto& e : c->ev_done) ZK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& e : c->ev_acc) ZK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     return c.release();
   } catch (...) {
     return nullptr;
@@ -82,6 +83,7 @@ void zk_ctx_destroy(zk_ctx* ctx) {
   (void)hipEventDestroy(ctx->ev_scal);
   (void)hipEventDestroy(ctx->ev_hsort);
   for (auto& e : ctx->ev_done) (void)hipEventDestroy(e);
+  for (auto& e : ctx->ev_acc) (void)hipEventDestroy(e);
   delete ctx;
 }
 

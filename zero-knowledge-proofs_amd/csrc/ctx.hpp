@@ -31,6 +31,7 @@ struct zk_ctx {
   hipStream_t side[zk::NUM_SIDE] = {};          // G2 / IC / A+B1 MSM streams
   hipEvent_t ev_quot = nullptr, ev_scal = nullptr, ev_hsort = nullptr;
   hipEvent_t ev_done[zk::NUM_MSM] = {};         // per-MSM completion (results downloaded)
+  hipEvent_t ev_acc[zk::NUM_MSM] = {};          // per-MSM accumulate done (chained schedule 8)
   std::string err;
   zk::MsmWork msm[zk::NUM_MSM];
   std::map<uint32_t, std::unique_ptr<zk::NttDomain>> domains;

@@ -1138,6 +1138,7 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
     ZK_LAUNCH_CHECK();
     if (pf) pf->end(st, ph);
   }
+  if (w.accum_done) ZK_HIP(hipEventRecord(w.accum_done, st));   // the next accumulate in a chain may start
   ph = pf ? pf->begin(st, (w.tag + "msm_merge").c_str(), p.G) : -1;   // buckets split across chunks
   w.nbig.ensure(sizeof(uint32_t));
   ZK_HIP(hipMemsetAsync(w.nbig.p, 0, sizeof(uint32_t), st));

@@ -97,7 +97,8 @@ struct MsmWork {
   Prof* prof = nullptr;  // optional live kernel timing
   hipEvent_t accum_wait = nullptr;   // if set, the accumulate kernel waits for this event
   hipEvent_t sort_done = nullptr;    // if set, recorded once the entries are grouped by bucket
-  std::string tag;       // phase-name prefix (per-MSM profiling)
+  hipEvent_t accum_done = nullptr;   // if set, recorded once the accumulate kernel has run
+  std::string tag;      // phase-name prefix (per-MSM profiling)
 };
 
 // Launch the device part of an MSM over n Montgomery-affine device bases and

@@ -570,8 +570,51 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
     for (int sl = 0; sl < NUM_MSM; sl++) {
       ctx->msm[sl].accum_wait = nullptr;
       ctx->msm[sl].sort_done = nullptr;
+      ctx->msm[sl].accum_done = nullptr;
     }
-    if (sched >= 4 && sched <= 7) run_quotient();
+    if (sched >= 4 && sched <= 8) run_quotient();
+    // 8: the quotient first, then the accumulates one after another in
+    // ZK_ACCUM_ORDER ('H' the H group, '2' the G2 MSM, 'A' the other G1
+    // groups; default "H2A"): every sort still starts with the witness, and
+    // each MSM's latency-bound tail (merge, bucket sums) overlaps the next
+    // accumulate instead of three full-occupancy rounds fighting for the chip.
+    if (sched == 8) {
+      static const std::string order = [] {
+        const char* e = getenv("ZK_ACCUM_ORDER");
+        std::string o = e ? e : "H2A";
+        std::string s = o;
+        std::sort(s.begin(), s.end());
+        return s == "2AH" ? o : std::string("H2A");
+      }();
+      ZK_HIP(hipEventRecord(ctx->ev_quot, st));
+      ctx->flags_host.ensure(16);
+      ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
+      hipEvent_t prev = ctx->ev_quot;
+      int side = 1;
+      for (char u : order) {
+        if (u == '2') {
+          MsmWork& w = ctx->msm[MSM_B2];
+          w.accum_wait = prev;
+          w.accum_done = prev = ctx->ev_acc[MSM_B2];
+          ZK_HIP(hipStreamWaitEvent(s2, ctx->ev_scal, 0));
+          launch_slot(MSM_B2, s2);
+          continue;
+        }
+        for (const auto& grp : groups) {
+          if (has_h(grp) != (u == 'H')) continue;
+          MsmWork& w = ctx->msm[grp[0]];
+          w.accum_wait = (u == 'H' && prev == ctx->ev_quot) ? nullptr : prev;   // H: same stream as the quotient
+          w.accum_done = prev = ctx->ev_acc[grp[0]];
+          hipStream_t gs = st;
+          if (u != 'H') {
+            gs = ctx->side[side];
+            side = side + 1 < NUM_SIDE ? side + 1 : 1;
+            ZK_HIP(hipStreamWaitEvent(gs, ctx->ev_scal, 0));
+          }
+          launch_group(grp, gs);
+        }
+      }
+    }
     if (sched == 5) {
       ZK_HIP(hipEventRecord(ctx->ev_quot, st));
       for (int sl = 0; sl < NUM_MSM; sl++) ctx->msm[sl].accum_wait = sl == MSM_H ? nullptr : ctx->ev_quot;
@@ -592,7 +635,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
     // the G2 MSM starts with the witness (ZK_PROVE_SCHED=1: after the quotient, below)
     if (sched == 3) {
       launch_slot(MSM_B2, st);
-    } else if (sched != 1) {
+    } else if (sched != 1 && sched != 8) {
       ZK_HIP(hipStreamWaitEvent(s2, ctx->ev_scal, 0));
       launch_slot(MSM_B2, s2);
     }
@@ -600,7 +643,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
     int side = 1;
     std::vector<hipStream_t> used;
     for (const auto& grp : groups) {
-      if (has_h(grp)) continue;
+      if (has_h(grp) || sched == 8) continue;
       hipStream_t gs = st;
       if (sched != 3) {
         gs = ctx->side[side];
@@ -610,7 +653,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       }
       launch_group(grp, gs);
     }
-    if (sched < 4 || sched > 7) run_quotient();
+    if (sched < 4 || sched > 8) run_quotient();
     if (sched == 1) {
       ZK_HIP(hipEventRecord(ctx->ev_quot, st));
       ZK_HIP(hipStreamWaitEvent(s2, ctx->ev_quot, 0));
@@ -618,7 +661,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
     }
     ZK_HIP(hipEventRecord(ctx->ev_done[MSM_B2], s2));
     waits.push_back(MSM_B2);
-    if (sched != 6 && sched != 7) {
+    if (sched != 6 && sched != 7 && sched != 8) {
       ctx->flags_host.ensure(16);
       ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
       for (const auto& grp : groups)
@@ -699,6 +742,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   for (int sl = 0; sl < NUM_MSM; sl++) {
     ctx->msm[sl].accum_wait = nullptr;
     ctx->msm[sl].sort_done = nullptr;
+    ctx->msm[sl].accum_done = nullptr;
   }
   ctx->prof.add_host("host_finish", t_fin);
   ctx->prof.collect();

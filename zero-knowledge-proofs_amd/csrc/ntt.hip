@@ -127,6 +127,7 @@ struct PassIO {
   const Fr* stab;
   Fr scale;
   uint32_t flags;
+  uint64_t gmask = ~0ull;   // ZK_NTT_EXPMASK (experiment only, wrong results): confine HBM indices
 };
 
 // One pass = one four-step level.  The block of N = 2^(s_lo+ns) elements
@@ -162,7 +163,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(PassIO io, NttTabs tab
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) {
     const uint32_t r = k >> logC, c = k & (C - 1);
     const size_t gi = base + ((size_t)r << s_lo) + c;
-    const size_t si = gather ? bitrev32((uint32_t)gi, log_n) : gi;
+    const size_t si = (gather ? bitrev32((uint32_t)gi, log_n) : gi) & io.gmask;
     Fr v = ld_vec(&io.src[si]);
     if (io.ltab) v = fp_mul(v, ld_vec(&io.ltab[si]));
     if (DIT && s_lo) v = fp_mul(v, tw_full(tabs, ((lo0 + c) * bitrev32(r, ns)) << tw_shift, log_n));
@@ -172,7 +173,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(PassIO io, NttTabs tab
   ntt_rounds<DIT>(sh, tabs.sm, ns, logC);
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) {
     const uint32_t r = k >> logC, c = k & (C - 1);
-    const size_t go = base + ((size_t)r << s_lo) + c;
+    const size_t go = (base + ((size_t)r << s_lo) + c) & io.gmask;
     Fr v = ld_vec(&sh[k]);
     if (!DIT && s_lo) v = fp_mul(v, tw_full(tabs, ((lo0 + c) * bitrev32(r, ns)) << tw_shift, log_n));
     if (io.stab) v = fp_mul(v, ld_vec(&io.stab[go]));
@@ -181,8 +182,14 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(PassIO io, NttTabs tab
   }
 }
 
-static void run_pass_io(bool dit, const PassIO& io, const NttTabs& t, uint32_t log_n, uint32_t s_lo, uint32_t ns,
+static void run_pass_io(bool dit, const PassIO& io_in, const NttTabs& t, uint32_t log_n, uint32_t s_lo, uint32_t ns,
                         hipStream_t st) {
+  static const uint64_t gmask = [] {
+    const char* e = getenv("ZK_NTT_EXPMASK");
+    return e ? strtoull(e, nullptr, 0) : ~0ull;
+  }();
+  PassIO io = io_in;
+  io.gmask = gmask;
   const uint32_t logC = std::min<uint32_t>(s_lo, NTT_TILE_LOG - ns);
   const uint32_t tiles = (uint32_t)((1ull << log_n) >> (ns + logC));
   const size_t lds = sizeof(Fr) << (ns + logC);

@@ -124,8 +124,9 @@ const char *zk_build_id(void);
  * 3 every kernel in order on one stream (isolated kernel durations), 4
  * quotient queued first, 5 and 6 accumulates held for the quotient / the H
  * sort, 7 as 6 with the G2 accumulate free, 8 the accumulates chained one
- * after another (ZK_ACCUM_ORDER).  Results never depend on it.
- * ZK_ERR_ARG outside -1..8.  No reference counterpart. */
+ * after another (ZK_ACCUM_ORDER), 9 as 0 with the G2 accumulate held until
+ * the G1 groups are sorted.  Results never depend on it.
+ * ZK_ERR_ARG outside -1..9.  No reference counterpart. */
 int zk_ctx_set_schedule(zk_ctx *ctx, int schedule);
 
 /* ---------------------------------------------------------------- MSM --- */

@@ -188,7 +188,7 @@ def test_schedules_give_the_same_proof(ctx, zkp, oracle, log_n):
     assert rc == 0
     dpk = zkp.CRS.generate_device(ctx, qap, zkp.SetupParams(*params), 1)
     try:
-        for sched in (0, 1, 3, 4, 5, 6, 7, 8, -1):
+        for sched in (0, 1, 3, 4, 5, 6, 7, 8, 9, -1):
             ctx.set_schedule(sched)
             p = zkp.Prover.prove_device(dpk, z.data_ptr(), len(zh), 1, r, s)
             torch.cuda.synchronize()

@@ -299,13 +299,14 @@ void ntt_natural(Fr* dst, const Fr* src, Fr* tmp, const NttDomain& dom, bool inv
 // iNTT -> coset shift -> NTT (the quotient's per-polynomial round trip):
 // the last DIF pass and the first DIT pass both work on the same contiguous
 // 2^ns-element tiles, so ONE kernel runs the DIF stages with the inverse
-// twiddles, multiplies each element p by tab[bitrev(p)] (n^-1 g^i) and runs
+// twiddles, multiplies each element p by tab_br[p] = n^-1 g^bitrev(p) (a
+// contiguous read: gathering tab[bitrev(p)] from an n-entry table touched a
+// new 128-B line and, beyond the MALL, a new page per element) and runs
 // the DIT stages with the forward twiddles while the tile stays in LDS: two
 // HBM round trips and the separate scale pass disappear.
 __global__ void __launch_bounds__(NTT_THREADS) k_ntt_tile_shift(Fr* __restrict__ data, const Fr* __restrict__ ism,
                                                                const Fr* __restrict__ sm,
-                                                               const Fr* __restrict__ tab, uint32_t log_n,
-                                                               uint32_t ns) {
+                                                               const Fr* __restrict__ tab_br, uint32_t ns) {
   extern __shared__ uint4 sh_raw[];
   Fr* sh = reinterpret_cast<Fr*>(sh_raw);
   const uint32_t tile_elems = 1u << ns;
@@ -314,18 +315,17 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_tile_shift(Fr* __restrict__
   __syncthreads();
   ntt_rounds<false>(sh, ism, ns, 0);
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) {
-    const uint32_t p = (uint32_t)(base + k);
-    st_vec(&sh[k], fp_mul(ld_vec(&sh[k]), ld_vec(&tab[bitrev32(p, log_n)])));
+    st_vec(&sh[k], fp_mul(ld_vec(&sh[k]), ld_vec(&tab_br[base + k])));
   }
   __syncthreads();
   ntt_rounds<true>(sh, sm, ns, 0);
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) st_vec(&data[base + k], ld_vec(&sh[k]));
 }
 
-void ntt_coset_shift(Fr* d, const NttDomain& dom, const Fr* tab, hipStream_t st, Prof* pf) {
+void ntt_coset_shift(Fr* d, const NttDomain& dom, const Fr* tab_br, hipStream_t st, Prof* pf) {
   const uint32_t L = dom.log_n;
   if (L == 0) {
-    fr_scale_table(d, tab, 0, true, st);
+    fr_scale_table(d, tab_br, 0, false, st);
     return;
   }
   const int ph = pf ? pf->begin(st, "ntt", (uint64_t)2 << L) : -1;
@@ -338,7 +338,7 @@ void ntt_coset_shift(Fr* d, const NttDomain& dom, const Fr* tab, hipStream_t st,
     s_hi -= plan[i];
   }
   const uint32_t ns = plan.back();   // s_hi == ns here: the contiguous pass
-  k_ntt_tile_shift<<<(uint32_t)((1ull << L) >> ns), NTT_THREADS, sizeof(Fr) << ns, st>>>(d, ti.sm, tf.sm, tab, L, ns);
+  k_ntt_tile_shift<<<(uint32_t)((1ull << L) >> ns), NTT_THREADS, sizeof(Fr) << ns, st>>>(d, ti.sm, tf.sm, tab_br, ns);
   ZK_LAUNCH_CHECK();
   // forward transform: every DIT pass but the first (contiguous) one
   uint32_t s_lo = ns;
@@ -421,6 +421,7 @@ void ntt_domain_init(NttDomain& d, uint32_t log_n, hipStream_t st) {
   d.ith.ensure(sizeof(Fr) * nth);
   d.gpow.ensure(sizeof(Fr) * n);
   d.gipow.ensure(sizeof(Fr) * n);
+  d.gpow_br.ensure(sizeof(Fr) * n);
   Fr one = fr_const(FrParams::ONE);
   Fr ninv = fr_const(FR_INV_2K[log_n]);
   fr_powers(d.sm.as<Fr>(), fr_const(FR_ROOTS[NTT_SM_LOG]), one, nsm, st);
@@ -433,6 +434,7 @@ void ntt_domain_init(NttDomain& d, uint32_t log_n, hipStream_t st) {
   }
   fr_powers(d.gpow.as<Fr>(), fr_const(FR_GEN), ninv, n, st);
   fr_powers(d.gipow.as<Fr>(), fr_const(FR_GEN_INV), ninv, n, st);
+  fr_bitrev_scale(d.gpow.as<Fr>(), d.gpow_br.as<Fr>(), log_n, nullptr, nullptr, st);
   d.zinv.ensure(sizeof(Fr));
   k_coset_zinv<<<1, 1, 0, st>>>(d.zinv.as<Fr>(), log_n);
   ZK_LAUNCH_CHECK();

@@ -29,6 +29,7 @@ struct NttDomain {
   DevBuf tl, itl;   // omega_n^x, x < min(n, 4096)
   DevBuf th, ith;   // omega_n^(4096 y), y < n / 4096
   DevBuf gpow;    // n^-1 * g^i, i < n   (coset shift g = 7)
+  DevBuf gpow_br; // gpow in bit-reversed order: read contiguously by the quotient's coset shift
   DevBuf gipow;   // n^-1 * g^-i, i < n
   DevBuf zinv;    // (g^n - 1)^-1: 1/Z on the coset g<w>
 };
@@ -74,10 +75,12 @@ void ntt_dit(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_
 void ntt_natural(Fr* dst, const Fr* src, Fr* tmp, const NttDomain& dom, bool inverse_twiddles, hipStream_t st,
                  Prof* pf, const Fr* ltab, const Fr* stab, const Fr* scale);
 
-// d <- NTT(tab[bitrev(i)] * iNTT(d)) with the inverse DIF's last pass, the
+// d <- NTT(tab_br[p] * iNTT(d)) with the inverse DIF's last pass, the
 // scale and the forward DIT's first pass fused into one tile kernel (the
-// quotient's coefficients -> coset evaluations step; tab = n^-1 g^i).
-void ntt_coset_shift(Fr* d_data, const NttDomain& dom, const Fr* d_tab, hipStream_t st, Prof* pf = nullptr);
+// quotient's coefficients -> coset evaluations step).  tab_br is the factor
+// table in bit-reversed order (NttDomain::gpow_br: n^-1 g^bitrev(p)), so the
+// tile reads it contiguously instead of gathering 32-B words across n.
+void ntt_coset_shift(Fr* d_data, const NttDomain& dom, const Fr* d_tab_br, hipStream_t st, Prof* pf = nullptr);
 // Elementwise helpers
 void fr_to_mont(const uint64_t* d_canon, Fr* d_out, size_t n, hipStream_t st);
 void fr_from_mont(const Fr* d_in, uint64_t* d_canon, size_t n, hipStream_t st);

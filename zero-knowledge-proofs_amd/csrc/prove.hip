@@ -99,17 +99,13 @@ __global__ void __launch_bounds__(256) k_quot_pointwise(Fr* __restrict__ qa, con
   st_vec(&qa[i], fp_mul(t, ld_vec(zinv)));
 }
 
-__device__ __forceinline__ uint32_t brev(uint32_t x, uint32_t log_n) {
-  return log_n ? (__builtin_bitreverse32(x) >> (32 - log_n)) : 0;
-}
-
-// H_i = n^-1 g^-i * (bit-reversed iNTT output)[i], then lo64 (core:203-208)
-__global__ void __launch_bounds__(256) k_h_final(const Fr* __restrict__ hb, const Fr* __restrict__ gipow,
-                                                 uint32_t log_n, uint64_t* __restrict__ hlo) {
+// H_i (Montgomery, natural order, n^-1 g^-i already applied) -> lo64 of the
+// canonical value (core:203-208)
+__global__ void __launch_bounds__(256) k_h_lo64(const Fr* __restrict__ h, size_t n, uint64_t* __restrict__ hlo) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >> log_n) return;
-  Fr h = fp_from_mont(fp_mul(ld_vec(&hb[brev((uint32_t)i, log_n)]), ld_vec(&gipow[i])));
-  hlo[i] = (uint64_t)h.v[0] | ((uint64_t)h.v[1] << 32);
+  if (i >= n) return;
+  const Fr c = fp_from_mont(ld_vec(&h[i]));
+  hlo[i] = (uint64_t)c.v[0] | ((uint64_t)c.v[1] << 32);
 }
 
 // out[k] = low word of src[idx[k] / div] (div > 1: a distributed-quotient
@@ -376,12 +372,12 @@ static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipS
   }();
   for (int k = 0; k < 3; k++) {
     if (fuse) {
-      ntt_coset_shift(v[k], dom, dom.gpow.as<Fr>(), st, pf);
+      ntt_coset_shift(v[k], dom, dom.gpow_br.as<Fr>(), st, pf);
       continue;
     }
     ntt_dif(v[k], dom, /*inverse twiddles*/ true, st, pf);
     ph = pf->begin(st, "quotient_misc", n);
-    fr_scale_table(v[k], dom.gpow.as<Fr>(), pk->log_n, true, st);
+    fr_scale_table(v[k], dom.gpow_br.as<Fr>(), pk->log_n, false, st);
     pf->end(st, ph);
     ntt_dit(v[k], dom, false, st, pf);
   }
@@ -389,11 +385,21 @@ static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipS
   k_quot_pointwise<<<ceil_div(n, 256), 256, 0, st>>>(v[0], v[1], v[2], dom.zinv.as<Fr>(), n);
   ZK_LAUNCH_CHECK();
   pf->end(st, ph);
-  ntt_dif(v[0], dom, true, st, pf);
+  // coset iNTT in natural order (the bit reversal is the first pass's tiled
+  // gather, n^-1 g^-i fused into the last pass's store) into v[1], v[2] as
+  // the scratch: an element-wise bit-reversed gather of the DIF output read
+  // every 32-B element from a different line (and page, beyond the MALL)
+  Fr* h = v[1];
+  if (pk->log_n == 0) {   // a size-1 transform is the identity: only the factor
+    fr_scale_table(v[0], dom.gipow.as<Fr>(), 0, false, st);
+    h = v[0];
+  } else {
+    ntt_natural(v[1], v[0], v[2], dom, true, st, pf, nullptr, dom.gipow.as<Fr>(), nullptr);
+  }
   ph = pf->begin(st, "quotient_misc", n);
   ctx->scal[MSM_H].ensure(sizeof(uint64_t) * n);
   ctx->tmp_scal.ensure(sizeof(uint64_t) * n);
-  k_h_final<<<ceil_div(n, 256), 256, 0, st>>>(v[0], dom.gipow.as<Fr>(), pk->log_n, ctx->tmp_scal.as<uint64_t>());
+  k_h_lo64<<<ceil_div(n, 256), 256, 0, st>>>(h, n, ctx->tmp_scal.as<uint64_t>());
   ZK_LAUNCH_CHECK();
   pf->end(st, ph);
 }
@@ -635,13 +641,17 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
     // the G2 MSM starts with the witness (ZK_PROVE_SCHED=1: after the quotient, below)
     if (sched == 3) {
       launch_slot(MSM_B2, st);
-    } else if (sched != 1 && sched != 8) {
+    } else if (sched != 1 && sched != 8 && sched != 9) {
       ZK_HIP(hipStreamWaitEvent(s2, ctx->ev_scal, 0));
       launch_slot(MSM_B2, s2);
     }
     // groups without H start with the witness on side[1], side[2], ...
+    // 9: as 0, but the G2 accumulate waits until these groups' entries are
+    // sorted, so its full-occupancy round cannot starve their sorts (and
+    // with them the start of the largest accumulate).
     int side = 1;
     std::vector<hipStream_t> used;
+    hipEvent_t g1_sorted = nullptr;
     for (const auto& grp : groups) {
       if (has_h(grp) || sched == 8) continue;
       hipStream_t gs = st;
@@ -651,7 +661,13 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
         ZK_HIP(hipStreamWaitEvent(gs, ctx->ev_scal, 0));
         used.push_back(gs);
       }
+      if (sched == 9) ctx->msm[grp[0]].sort_done = g1_sorted = ctx->ev_acc[grp[0]];
       launch_group(grp, gs);
+    }
+    if (sched == 9) {
+      ZK_HIP(hipStreamWaitEvent(s2, ctx->ev_scal, 0));
+      ctx->msm[MSM_B2].accum_wait = g1_sorted;
+      launch_slot(MSM_B2, s2);
     }
     if (sched < 4 || sched > 8) run_quotient();
     if (sched == 1) {

@@ -25,6 +25,29 @@ def test_unfused_quotient_matches_oracle():
 
 
 @pytest.mark.timeout(300)
+def test_large_domain_quotient_path_matches_oracle():
+    """ZK_NTT_FUSE=0 ZK_H_NATURAL=1: the quotient path the library picks from
+    2^23 constraints up (separate iNTT / bit-reversed-table coset scale / NTT,
+    and the final coset iNTT in natural order through ntt_natural), forced
+    at 1-, 2- and 3-pass sizes including the size-1 domain."""
+    env = dict(os.environ, ZK_NTT_FUSE="0", ZK_H_NATURAL="1")
+    res = subprocess.run([sys.executable, os.path.join(HERE, "unfused_quotient_check.py"), "ZK_H_NATURAL=1", "0", "1",
+                          "11", "12", "21"], env=env, capture_output=True, text=True, timeout=280)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
+    assert res.stdout.count(" ok") == 5
+
+
+@pytest.mark.timeout(300)
+def test_natural_final_with_fused_shift_matches_oracle():
+    """ZK_H_NATURAL=1 with the fused coset shift (the two switches combine)."""
+    env = dict(os.environ, ZK_H_NATURAL="1")
+    res = subprocess.run([sys.executable, os.path.join(HERE, "unfused_quotient_check.py"), "ZK_H_NATURAL=1", "2",
+                          "13"], env=env, capture_output=True, text=True, timeout=280)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
+    assert res.stdout.count(" ok") == 2
+
+
+@pytest.mark.timeout(300)
 def test_lazy_accumulate_matches_oracle():
     """ZK_LAZY_ACCUM=1: the G1 bucket accumulate in csrc/lazy.hpp's redundant
     signed-limb Fq form (an opt-in experiment) against the oracle."""

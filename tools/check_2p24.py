@@ -70,7 +70,7 @@ def main():
            "components_equal": {"a": bool(np.array_equal(proof.words[:13], oproof[:13])),
                                 "b": bool(np.array_equal(proof.words[13:38], oproof[13:38])),
                                 "c": bool(np.array_equal(proof.words[38:], oproof[38:]))},
-           "ntt_fuse": os.environ.get("ZK_NTT_FUSE", "1"), "build_id": zkp.build_id()}
+           "ntt_fuse": os.environ.get("ZK_NTT_FUSE", "auto (fused below 2^23)"), "build_id": zkp.build_id()}
     print(json.dumps(rec), flush=True)
     if not exact:
         sys.exit(1)

@@ -99,6 +99,20 @@ __global__ void __launch_bounds__(256) k_quot_pointwise(Fr* __restrict__ qa, con
   st_vec(&qa[i], fp_mul(t, ld_vec(zinv)));
 }
 
+__device__ __forceinline__ uint32_t brev(uint32_t x, uint32_t log_n) {
+  return log_n ? (__builtin_bitreverse32(x) >> (32 - log_n)) : 0;
+}
+
+// H_i = n^-1 g^-i * (bit-reversed iNTT output)[i], then lo64 (core:203-208):
+// the element-wise gather path for domains that stay in the MALL
+__global__ void __launch_bounds__(256) k_h_final(const Fr* __restrict__ hb, const Fr* __restrict__ gipow,
+                                                 uint32_t log_n, uint64_t* __restrict__ hlo) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >> log_n) return;
+  Fr h = fp_from_mont(fp_mul(ld_vec(&hb[brev((uint32_t)i, log_n)]), ld_vec(&gipow[i])));
+  hlo[i] = (uint64_t)h.v[0] | ((uint64_t)h.v[1] << 32);
+}
+
 // H_i (Montgomery, natural order, n^-1 g^-i already applied) -> lo64 of the
 // canonical value (core:203-208)
 __global__ void __launch_bounds__(256) k_h_lo64(const Fr* __restrict__ h, size_t n, uint64_t* __restrict__ hlo) {
@@ -364,12 +378,22 @@ static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipS
   pf->end(st, ph);
   Fr* v[3] = {ctx->qa.as<Fr>(), ctx->qb.as<Fr>(), ctx->qc.as<Fr>()};
   // per polynomial: iNTT (coefficients * n, bit-reversed), * n^-1 g^i, NTT
-  // (evaluations on the coset g<w>, natural order) -- ZK_NTT_FUSE=0 runs the
-  // three steps as separate passes
-  static const bool fuse = [] {
-    const char* e = getenv("ZK_NTT_FUSE");
-    return !(e && std::strcmp(e, "0") == 0);
-  }();
+  // (evaluations on the coset g<w>, natural order).  Fused into one tile
+  // kernel below 2^LARGE_Q_LOG; from there the three steps run as separate
+  // passes, and the final coset iNTT runs in natural order (ntt_natural)
+  // instead of a DIF plus an element-wise bit-reversed gather.  Same-box
+  // A/B, overlapped prove: 2^24 fused 122.8 / separate 118.6 ms; 2^20 the
+  // gather path 9.89 / natural 10.01 ms (profiles/r02_ab_quot.txt).
+  // ZK_NTT_FUSE=0/1 and ZK_H_NATURAL=0/1 force either choice.
+  constexpr uint32_t LARGE_Q_LOG = 23;
+  auto env_or = [](const char* name) {
+    const char* e = getenv(name);
+    return e ? (std::strcmp(e, "0") == 0 ? 0 : 1) : -1;
+  };
+  static const int fuse_env = env_or("ZK_NTT_FUSE"), nat_env = env_or("ZK_H_NATURAL");
+  const bool large = pk->log_n >= LARGE_Q_LOG;
+  const bool fuse = fuse_env >= 0 ? fuse_env == 1 : !large;
+  const bool natural = nat_env >= 0 ? nat_env == 1 : large;
   for (int k = 0; k < 3; k++) {
     if (fuse) {
       ntt_coset_shift(v[k], dom, dom.gpow_br.as<Fr>(), st, pf);
@@ -385,10 +409,21 @@ static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipS
   k_quot_pointwise<<<ceil_div(n, 256), 256, 0, st>>>(v[0], v[1], v[2], dom.zinv.as<Fr>(), n);
   ZK_LAUNCH_CHECK();
   pf->end(st, ph);
-  // coset iNTT in natural order (the bit reversal is the first pass's tiled
-  // gather, n^-1 g^-i fused into the last pass's store) into v[1], v[2] as
-  // the scratch: an element-wise bit-reversed gather of the DIF output read
-  // every 32-B element from a different line (and page, beyond the MALL)
+  // coset iNTT: small domains run a DIF and gather its bit-reversed output
+  // element by element (k_h_final, all in the MALL); large ones run it in
+  // natural order (the bit reversal is the first pass's tiled gather,
+  // n^-1 g^-i fused into the last pass's store) into v[1], v[2] as scratch,
+  // since beyond the MALL every gathered 32-B element was its own line/page
+  ctx->scal[MSM_H].ensure(sizeof(uint64_t) * n);
+  ctx->tmp_scal.ensure(sizeof(uint64_t) * n);
+  if (!natural) {
+    ntt_dif(v[0], dom, true, st, pf);
+    ph = pf->begin(st, "quotient_misc", n);
+    k_h_final<<<ceil_div(n, 256), 256, 0, st>>>(v[0], dom.gipow.as<Fr>(), pk->log_n, ctx->tmp_scal.as<uint64_t>());
+    ZK_LAUNCH_CHECK();
+    pf->end(st, ph);
+    return;
+  }
   Fr* h = v[1];
   if (pk->log_n == 0) {   // a size-1 transform is the identity: only the factor
     fr_scale_table(v[0], dom.gipow.as<Fr>(), 0, false, st);
@@ -397,8 +432,6 @@ static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipS
     ntt_natural(v[1], v[0], v[2], dom, true, st, pf, nullptr, dom.gipow.as<Fr>(), nullptr);
   }
   ph = pf->begin(st, "quotient_misc", n);
-  ctx->scal[MSM_H].ensure(sizeof(uint64_t) * n);
-  ctx->tmp_scal.ensure(sizeof(uint64_t) * n);
   k_h_lo64<<<ceil_div(n, 256), 256, 0, st>>>(h, n, ctx->tmp_scal.as<uint64_t>());
   ZK_LAUNCH_CHECK();
   pf->end(st, ph);

@@ -56,10 +56,16 @@ zk_ctx* zk_ctx_create(int device) {
     int lo_prio = 0, hi_prio = 0;
     ZK_HIP(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
     ZK_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio));   // quotient + H
-    const char* g2p = getenv("ZK_G2_PRIO");   // tuning: "lo" puts the G2 stream at low priority
-    ZK_HIP(hipStreamCreateWithPriority(&c->side[0], hipStreamNonBlocking,
-                                       (g2p && g2p[0] == 'l') ? lo_prio : hi_prio));  // G2 MSM
-    for (int i = 1; i < NUM_SIDE; i++) ZK_HIP(hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking, lo_prio));
+    // side[0]: G2 MSM (high), side[1..]: the G1 groups (low).  Tuning:
+    // ZK_G2_PRIO=lo puts the G2 stream low; ZK_SIDE_PRIO lists h/l per side
+    // stream (e.g. "hhl") and overrides both.
+    const char* g2p = getenv("ZK_G2_PRIO");
+    const char* sp = getenv("ZK_SIDE_PRIO");
+    for (int i = 0; i < NUM_SIDE; i++) {
+      bool hi = i == 0 ? !(g2p && g2p[0] == 'l') : false;
+      if (sp && (int)std::strlen(sp) > i) hi = sp[i] == 'h';
+      ZK_HIP(hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking, hi ? hi_prio : lo_prio));
+    }
     ZK_HIP(hipEventCreateWithFlags(&c->ev_quot, hipEventDisableTiming));
     ZK_HIP(hipEventCreateWithFlags(&c->ev_scal, hipEventDisableTiming));
     ZK_HIP(hipEventCreateWithFlags(&c->ev_hsort, hipEventDisableTiming));

@@ -139,42 +139,54 @@ ZK_DI XYZZ<F> xyzz_madd(const XYZZ<F>& p, const Affine<F>& a) {
 // add-2008-s: p + q.  Operations are ordered so that each input coordinate
 // dies as early as possible (G2 points are 96 VGPRs each; the textbook order
 // keeps both points and four products live at once and spills).
-template <class F>
-ZK_DI XYZZ<F> xyzz_add(const XYZZ<F>& p, const XYZZ<F>& q) {
+template <class F, bool SB>
+ZK_DI XYZZ<F> xyzz_add_impl(const XYZZ<F>& p, const XYZZ<F>& q) {
   if (xyzz_is_inf(p)) return q;
   if (xyzz_is_inf(q)) return p;
   F U1 = f_mul(p.X, q.ZZ);
-  ZK_SB();
+  if constexpr (SB) ZK_SB();
   F P = f_sub(f_mul(q.X, p.ZZ), U1);
-  ZK_SB();
+  if constexpr (SB) ZK_SB();
   F S1 = f_mul(p.Y, q.ZZZ);
-  ZK_SB();
+  if constexpr (SB) ZK_SB();
   F R = f_sub(f_mul(q.Y, p.ZZZ), S1);
-  ZK_SB();
+  if constexpr (SB) ZK_SB();
   if (f_is_zero(P)) {
     if (f_is_zero(R)) return xyzz_dbl_call(p);
     XYZZ<F> r; xyzz_set_inf(r); return r;
   }
   XYZZ<F> r;
   F PP = f_sqr(P);
-  ZK_SB();
+  if constexpr (SB) ZK_SB();
   r.ZZ = f_mul(p.ZZ, q.ZZ);
-  ZK_SB();
+  if constexpr (SB) ZK_SB();
   r.ZZ = f_mul(r.ZZ, PP);
-  ZK_SB();
+  if constexpr (SB) ZK_SB();
   F PPP = f_mul(P, PP);
-  ZK_SB();
+  if constexpr (SB) ZK_SB();
   r.ZZZ = f_mul(p.ZZZ, q.ZZZ);
-  ZK_SB();
+  if constexpr (SB) ZK_SB();
   r.ZZZ = f_mul(r.ZZZ, PPP);
-  ZK_SB();
+  if constexpr (SB) ZK_SB();
   F Q = f_mul(U1, PP);
-  ZK_SB();
+  if constexpr (SB) ZK_SB();
   r.X = f_sub(f_sub(f_sqr(R), PPP), f_add(Q, Q));
-  ZK_SB();
+  if constexpr (SB) ZK_SB();
   r.Y = f_mul_sub(R, f_sub(Q, r.X), S1, PPP);
-  ZK_SB();
+  if constexpr (SB) ZK_SB();
   return r;
+}
+template <class F>
+ZK_DI XYZZ<F> xyzz_add(const XYZZ<F>& p, const XYZZ<F>& q) {
+  return xyzz_add_impl<F, true>(p, q);
+}
+// The same add with the scheduler free to overlap its independent products
+// (U1 / U2 / S1 / S2, the ZZ and ZZZ chains): for the latency-bound G1
+// reduction kernels (fixup, row/column sums) that run one or two waves per
+// SIMD, where the serial product chain, not the VGPR count, sets the time.
+template <class F>
+ZK_DI XYZZ<F> xyzz_add_ilp(const XYZZ<F>& p, const XYZZ<F>& q) {
+  return xyzz_add_impl<F, false>(p, q);
 }
 
 // ---- lane-quad cooperative add (latency-bound reductions) --------------

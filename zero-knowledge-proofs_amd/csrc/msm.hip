@@ -583,6 +583,22 @@ static bool g2_pair_mode() {
 //    now complete and passes the rest up: log4(M/K) levels of <= 7 adds.
 constexpr int MSM_MERGE_FAN = 4;
 
+// The latency-bound G1 reductions (fixup, row/column sums, quantities) run
+// their adds without the scheduling barriers (xyzz_add_ilp); G2 keeps them
+// (its lane-pair points would spill).  ZK_TAIL_ILP=0 (build flag) restores
+// the barriers everywhere (A/B).
+#ifndef ZK_TAIL_ILP
+#define ZK_TAIL_ILP 1
+#endif
+template <class F>
+ZK_DI XYZZ<F> tail_add(const XYZZ<F>& p, const XYZZ<F>& q) {
+  return xyzz_add(p, q);
+}
+ZK_DI XYZZ<Fq> tail_add(const XYZZ<Fq>& p, const XYZZ<Fq>& q) {
+  if constexpr (ZK_TAIL_ILP != 0) return xyzz_add_ilp(p, q);
+  else return xyzz_add(p, q);
+}
+
 __device__ __forceinline__ bool big_bucket(const uint32_t* off, uint32_t b, uint32_t K, uint32_t fix_max) {
   return (off[b + 1] - 1) / K - off[b] / K + 1 > fix_max;
 }
@@ -604,8 +620,19 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
     return;
   }
   X acc = ld_vec(&partials[2 * (size_t)t0 + 1]);
-  for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, ld_vec(&partials[2 * (size_t)t]));
+  for (uint32_t t = t0 + 1; t <= t1; t++) acc = tail_add(acc, ld_vec(&partials[2 * (size_t)t]));
   st_vec(&buckets[g], acc);
+}
+
+template <class X>
+__device__ __forceinline__ X shfl_xor_point(const X& v, int d) {
+  constexpr int NW = sizeof(X) / 4;
+  X o;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&v);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+  for (int k = 0; k < NW; k++) dst[k] = __shfl_xor(src[k], d);
+  return o;
 }
 
 template <class C>
@@ -660,16 +687,6 @@ __global__ void __launch_bounds__(128) k_msm_merge(const uint32_t* __restrict__ 
 // step against ~20K instructions per add).  Both phases run through ONE
 // xyzz_add call site: the loop is not unrolled, so the kernel's code stays
 // a single add (I-cache) instead of 1 + 6 inlined copies.
-template <class X>
-__device__ __forceinline__ X shfl_xor_point(const X& v, int d) {
-  constexpr int NW = sizeof(X) / 4;
-  X o;
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(&v);
-  uint32_t* dst = reinterpret_cast<uint32_t*>(&o);
-#pragma unroll
-  for (int k = 0; k < NW; k++) dst[k] = __shfl_xor(src[k], d);
-  return o;
-}
 
 constexpr int MSM_RED_WAVES = 4;   // sums per 256-thread workgroup
 
@@ -706,7 +723,7 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_rowcol(MsmPlan p, co
     } else {
       o = shfl_xor_point(v, 1 << (it - niter));
     }
-    v = xyzz_add(v, o);
+    v = tail_add(v, o);
   }
   if (lane == 0) st_vec(&rc[b], v);
 }
@@ -747,7 +764,7 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_quant(MsmPlan p, con
     } else {
       o = shfl_xor_point(v, 1 << (it - niter));
     }
-    v = xyzz_add(v, o);
+    v = tail_add(v, o);
   }
   if (lane == 0) st_vec(&res[b], v);
 }

@@ -583,10 +583,11 @@ static bool g2_pair_mode() {
 //    now complete and passes the rest up: log4(M/K) levels of <= 7 adds.
 constexpr int MSM_MERGE_FAN = 4;
 
-// The latency-bound G1 reductions (fixup, row/column sums, quantities) run
-// their adds without the scheduling barriers (xyzz_add_ilp); G2 keeps them
-// (its lane-pair points would spill).  ZK_TAIL_ILP=0 (build flag) restores
-// the barriers everywhere (A/B).
+// The latency-bound G1 reductions (fixup, row/column sums, quantities, the
+// tree merge) run their adds without the scheduling barriers
+// (xyzz_add_ilp), so independent products overlap; ZK_TAIL_ILP=0 (build
+// flag) restores them (A/B).  The one-lane G2 path keeps them (its 96-VGPR
+// points would spill).
 #ifndef ZK_TAIL_ILP
 #define ZK_TAIL_ILP 1
 #endif
@@ -596,6 +597,18 @@ ZK_DI XYZZ<F> tail_add(const XYZZ<F>& p, const XYZZ<F>& q) {
 }
 ZK_DI XYZZ<Fq> tail_add(const XYZZ<Fq>& p, const XYZZ<Fq>& q) {
   if constexpr (ZK_TAIL_ILP != 0) return xyzz_add_ilp(p, q);
+  else return xyzz_add(p, q);
+}
+// G2 lane-pair sums (row/column sums, fixup) as well: prove 9.61 -> 9.55 ms
+// (median of 5 alternating pairs, profiles/r02_ab_g2_ilp.txt; the 408 B of
+// scratch are the out-of-line doubling call, with or without); ZK_TAIL_ILP_G2=0
+// (build flag) keeps their barriers
+
+#ifndef ZK_TAIL_ILP_G2
+#define ZK_TAIL_ILP_G2 1
+#endif
+ZK_DI XYZZ<Fq2h> tail_add(const XYZZ<Fq2h>& p, const XYZZ<Fq2h>& q) {
+  if constexpr (ZK_TAIL_ILP_G2 != 0) return xyzz_add_ilp(p, q);
   else return xyzz_add(p, q);
 }
 
@@ -672,7 +685,7 @@ __global__ void __launch_bounds__(128) k_msm_merge(const uint32_t* __restrict__ 
   while (k < ns) {
     const uint32_t b = sb[k];
     X acc = ld_vec(&in[si[k]]);
-    for (k++; k < ns && sb[k] == b; k++) acc = xyzz_add(acc, ld_vec(&in[si[k]]));
+    for (k++; k < ns && sb[k] == b; k++) acc = tail_add(acc, ld_vec(&in[si[k]]));
     if (off[b] >= s && off[b + 1] <= e) st_vec(&buckets[b], acc);   // complete
     else if (off[b] < s) st_vec(&out[2 * (size_t)u], acc);           // open at the start
     else st_vec(&out[2 * (size_t)u + 1], acc);                       // open at the end
@@ -956,7 +969,7 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_rowcol_pair(MsmPlan 
     } else {
       o = shfl_xor_point(v, 2 << (it - niter));
     }
-    v = xyzz_add(v, o);
+    v = tail_add(v, o);
   }
   if ((threadIdx.x & 63) < 2) st_pair(&rc[b], v);
 }
@@ -977,7 +990,7 @@ __global__ void __launch_bounds__(128) k_msm_fixup_pair(const uint32_t* __restri
   }
   XYZZ<Fq2h> acc = ld_pair(&partials[2 * (size_t)t0 + 1]);
 #pragma unroll 1
-  for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, ld_pair(&partials[2 * (size_t)t]));
+  for (uint32_t t = t0 + 1; t <= t1; t++) acc = tail_add(acc, ld_pair(&partials[2 * (size_t)t]));
   st_pair(&buckets[g], acc);
 }
 

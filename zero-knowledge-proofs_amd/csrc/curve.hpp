@@ -11,6 +11,8 @@
 // Device affine layout: Montgomery x then y, (0,0) = point at infinity
 // (0 != 4 so (0,0) is off-curve for both groups).
 #pragma once
+#include <type_traits>
+
 #include "ff.hpp"
 
 // Scheduling barrier between field operations: keeps the scheduler from
@@ -152,7 +154,12 @@ ZK_DI XYZZ<F> xyzz_add_impl(const XYZZ<F>& p, const XYZZ<F>& q) {
   F R = f_sub(f_mul(q.Y, p.ZZZ), S1);
   if constexpr (SB) ZK_SB();
   if (f_is_zero(P)) {
-    if (f_is_zero(R)) return xyzz_dbl_call(p);
+    if (f_is_zero(R)) {
+      // inline for the G1 reductions (no call frame: their kernels then need
+      // no scratch); out of line elsewhere (live-set pressure)
+      if constexpr (!SB && std::is_same<F, Fq>::value) return xyzz_dbl(p);
+      else return xyzz_dbl_call(p);
+    }
     XYZZ<F> r; xyzz_set_inf(r); return r;
   }
   XYZZ<F> r;

@@ -104,7 +104,8 @@ const char *zk_last_error(const zk_ctx *ctx);
 int zk_ctx_synchronize(zk_ctx *ctx);
 /* Live kernel timing: HIP events recorded on the launching stream around
  * each kernel phase (msm_sort, msm_accum_g1, msm_accum_g2, msm_merge,
- * msm_bucket_sum, ntt, quotient_eval, quotient_misc).  No reference
+ * msm_bucket_sum, ntt, quotient_eval, quotient_misc).  enable: 0 off (and
+ * clear), 1 on, 2 on plus a per-launch stream timeline.  No reference
  * counterpart (measurement). */
 int zk_ctx_profile(zk_ctx *ctx, int enable);
 /* names: '\0'-separated phase names; per phase: total ms, launches, work
@@ -112,6 +113,11 @@ int zk_ctx_profile(zk_ctx *ctx, int enable);
 int zk_ctx_profile_read(zk_ctx *ctx, char *names, size_t names_cap, double *ms,
                         uint64_t *launches, uint64_t *units, size_t max_phases,
                         size_t *nphases);
+/* The timeline of zk_ctx_profile(ctx, 2): one text line per profiled launch
+ * ("phase stream start_ms end_ms", times from the start of its proof) and
+ * "--" after each proof.  *len = its length; with buf (cap > len) the text is
+ * copied NUL-terminated and the timeline cleared. */
+int zk_ctx_timeline_read(zk_ctx *ctx, char *buf, size_t cap, size_t *len);
 
 /* Build provenance: "<git HEAD>[-dirty] src:<16 hex of sha256 over the
  * sources in zero-knowledge-proofs_amd/csrc/ *.hip and *.hpp (sorted) and
@@ -119,15 +125,36 @@ int zk_ctx_profile_read(zk_ctx *ctx, char *names, size_t names_cap, double *ms,
  * the tree it runs in and refuses a library built from other sources.  No
  * reference counterpart. */
 const char *zk_build_id(void);
-/* Prove stream schedule (measurement): -1 default (ZK_PROVE_SCHED or the
- * overlapped four-stream schedule), 0 overlapped, 1 G2 after the quotient,
- * 3 every kernel in order on one stream (isolated kernel durations), 4
- * quotient queued first, 5 and 6 accumulates held for the quotient / the H
- * sort, 7 as 6 with the G2 accumulate free, 8 the accumulates chained one
- * after another (ZK_ACCUM_ORDER), 9 as 0 with the G2 accumulate held until
- * the G1 groups are sorted.  Results never depend on it.
- * ZK_ERR_ARG outside -1..9.  No reference counterpart. */
+/* Prove stream schedule (measurement): -1 or 0 the overlapped four-stream
+ * schedule (default), 3 every kernel in order on one stream (isolated kernel
+ * durations).  Results never depend on it.  ZK_ERR_ARG for anything else.
+ * No reference counterpart. */
 int zk_ctx_set_schedule(zk_ctx *ctx, int schedule);
+
+/* Explicit path choices of a ctx, for tests and A/B measurement.  The
+ * library reads nothing from the environment; without these calls it picks
+ * by size.  No value changes a result: each is covered by a bit-exact GPU
+ * test.  ZK_ERR_ARG for an unknown option or value.  No reference
+ * counterpart.
+ *   ZK_OPT_QUOTIENT_PATH  -1 by domain size (default: small-domain below
+ *                         2^23), 0 small-domain (fused iNTT/coset/NTT tile
+ *                         kernel, gathered final), 1 large-domain (separate
+ *                         passes, natural-order final coset iNTT)
+ *   ZK_OPT_PROVE_WIN_C    0 by size (default: 16, or 22 from 2^24 constraints
+ *                         per key shard), 16 or 22: digit window width of
+ *                         the prove MSMs of keys uploaded / set up after the
+ *                         call
+ *   ZK_OPT_EXCHANGE_TIMEOUT_MS  watchdog of the attached exchange (default
+ *                         60000, >= 1): a distributed-quotient proof whose
+ *                         peers do not answer within it fails with
+ *                         ZK_ERR_RCCL and aborts the exchange
+ *   ZK_OPT_FAULT_AFTER_EXCHANGE  test hook, 0 (default) or 1..3: the next
+ *                         distributed-quotient proof on this ctx fails right
+ *                         after its k-th all-to-all, as a rank-local error
+ *                         would (tests of the abort path) */
+enum { ZK_OPT_QUOTIENT_PATH = 1, ZK_OPT_PROVE_WIN_C = 2, ZK_OPT_EXCHANGE_TIMEOUT_MS = 3,
+       ZK_OPT_FAULT_AFTER_EXCHANGE = 4 };
+int zk_ctx_set_option(zk_ctx *ctx, int option, int64_t value);
 
 /* ---------------------------------------------------------------- MSM --- */
 /* Sum_i scalars[i] * bases[i], normalised to affine.  Replaces
@@ -218,7 +245,10 @@ int zk_groth16_prove_dev(zk_ctx *ctx, const zk_pk_dev *pk, const void *d_z, size
 
 /* ---- multi-GPU: MSM sharded by base range (one process per GPU) ---- */
 /* Upload only shard `shard` of `nshards` contiguous ranges of every base
- * vector (the QAP stays whole: the quotient is replicated per GPU). */
+ * vector (and the H bases i = shard mod nshards).  The constraint system
+ * stays whole on every rank: each computes the whole quotient unless its ctx
+ * is attached to an exchange of the key's (shard, nshards), in which case
+ * the quotient is distributed (zk_ctx_attach_rccl below). */
 int zk_pk_upload_shard(zk_ctx *ctx, const zk_pk *pk, const zk_r1cs_csr *qap,
                        uint32_t shard, uint32_t nshards, zk_pk_dev **out);
 int zk_groth16_setup_dev_shard(zk_ctx *ctx, const zk_r1cs_csr *qap, const zk_setup_params *params,
@@ -231,6 +261,23 @@ typedef struct { uint8_t bytes[ZK_PARTIAL_BYTES]; } zk_prove_partial;
 int zk_groth16_prove_partial(zk_ctx *ctx, const zk_pk_dev *pk_shard, const void *d_z, size_t zlen,
                              size_t num_public, const zk_fr *r, const zk_fr *s,
                              zk_prove_partial *out);
+/* The witness entries a key shard reads on this ctx: *nranges half-open
+ * index ranges [ranges[2k], ranges[2k+1]) of z, ascending and disjoint (at
+ * most cap are written).  With a distributed quotient (an exchange of the
+ * key's shape attached) that is z_0, the variables of the shard's MSM bases
+ * and those its quotient rows reference -- about 2/N of the witness for N
+ * shards; otherwise all of [0, zlen).  No reference counterpart. */
+int zk_groth16_witness_ranges(zk_ctx *ctx, const zk_pk_dev *pk_shard, uint64_t *ranges, size_t cap,
+                              size_t *nranges);
+/* zk_groth16_prove_partial from a HOST witness slice -- the sharded form of
+ * the drop-in prove(pk, witness, rng) (crates/groth16-core/src/lib.rs:139-147),
+ * each rank receiving only its part: z_slice holds z[lo..hi) of every range
+ * of zk_groth16_witness_ranges, concatenated in order (slice_len entries in
+ * all, else ZK_ERR_ARG); zlen is the length of the whole witness (the
+ * Witness::validate length check, core:113-118). */
+int zk_groth16_prove_partial_host(zk_ctx *ctx, const zk_pk_dev *pk_shard, const zk_fr *z_slice,
+                                  size_t slice_len, size_t zlen, size_t num_public, const zk_fr *r,
+                                  const zk_fr *s, zk_prove_partial *out);
 int zk_groth16_prove_combine(const zk_prove_partial *parts, size_t nparts,
                              const zk_fr *r, const zk_fr *s, zk_proof *out);
 
@@ -244,6 +291,24 @@ int zk_groth16_prove_combine(const zk_prove_partial *parts, size_t nparts,
  * the whole quotient.  No reference counterpart (multi-GPU). */
 int zk_rccl_unique_id(uint8_t out[128]);   /* one rank makes it, all attach with it */
 int zk_ctx_attach_rccl(zk_ctx *ctx, const uint8_t unique_id[128], int rank, int world);
+/* The same distributed quotient over a host-staged exchange: each of the
+ * three all-to-alls brings this rank's world chunks of chunk_bytes (chunk k
+ * for rank k) to pinned host memory and calls all_to_all, which must fill
+ * recv (chunk s from rank s) through the caller's transport -- e.g.
+ * torch.distributed over gloo, or any network -- and return 0;
+ * all_reduce_max replaces *value by its maximum over the ranks (the status
+ * agreement before the first exchange).  Non-zero from either callback ->
+ * ZK_ERR_RCCL.  abort (may be NULL) is called when this rank fails after
+ * the ranks agreed to start, so the caller can make its peers' pending
+ * transfers fail (e.g. by tearing the process group down).  Callbacks run on
+ * the thread that called the prove.  No reference counterpart. */
+typedef struct {
+  int (*all_to_all)(void *user, const void *send, void *recv, size_t chunk_bytes);
+  int (*all_reduce_max)(void *user, int32_t *value);
+  void (*abort)(void *user);
+  void *user;
+} zk_exchange_ops;
+int zk_ctx_attach_exchange(zk_ctx *ctx, const zk_exchange_ops *ops, int rank, int world);
 /* Diagnostic: nshards virtual ranks of one key on this ctx's single device
  * (the all-to-alls become device copies) -- checks the distributed path's
  * arithmetic and index maps without N devices. */

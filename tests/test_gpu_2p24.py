@@ -1,0 +1,103 @@
+"""configs[4] at size: the 2^24-constraint synthetic circuit
+(crates/groth16-cli/src/lib.rs:55-70, num_public = 1) proved three ways on
+ONE GPU, each bit for bit against the C oracle's prove() on the same
+pk / z / r / s (crates/groth16-core/src/lib.rs:139-272):
+
+  (a) the single-GPU proof: GPU setup straight into HBM, the c = 22
+      three-window plan and the large-domain quotient the library picks at
+      this size;
+  (b) 8 virtual shards (zk_test_prove_virtual_shards): the 8-GPU layout --
+      per-shard keys of 2^21 constraints (c = 16), the distributed quotient
+      at m = 2^21 with its real index maps, the three all-to-alls as device
+      copies, the MSM bases sharded by quotient-row ownership;
+  (c) the same 8 shard keys through zk_groth16_prove_partial (each rank
+      computing the whole quotient, no exchange) and zk_groth16_prove_combine.
+
+Seeds are bench.py's (setup params 0x5EED0001, witness 0x5EED0002), so the
+oracle's proof also equals the one recorded in profiles/r02_check_2p24_quot.json
+(ORACLE_2P24 below: the oracle is deterministic across rounds).  Each key is
+freed before the next is made.  Host memory: ~55 GB (the host key and the
+oracle's copy of it); GPU: ~70 GB for the 8 shard keys."""
+import os
+import sys
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+LOG_N = 24
+ORACLE_2P24 = ("975ca696ac5acaa2c7690b9d89ab763ee435fdae4fa76daf9d90e40e6c4cef0407dec0cf4b602165b475c26696cbec3e"
+               "a7ab7a7b36fda6704c05a6dedbb181099f278a050b96ebd2862da2a29bb0b436efb8cb355c2bb4c889dd0089e68a7d45"
+               "13db14b6f7322595e922f20c068400f5a044f3a4ce7311fec64d1f7e76ea24d68c1dd5328373c7369b56bd414eb6dea3"
+               "9583f11348f3813b597738ee46c4145abb606199f147e04bf4786b7fbe29b7e9646516e5f7dedf4535783d11ece4d9ce")
+
+
+def _bench():
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    return bench
+
+
+@pytest.fixture(scope="module")
+def case_2p24(ctx, zkp, oracle):
+    """(qap, params, r, s, device witness, oracle proof words) at 2^24."""
+    bench = _bench()
+    n = 1 << LOG_N
+    params, r, s = bench.setup_params(0x5EED0001)
+    qap = zkp.QAP(zkp.CSRMatrices.synthetic(n))
+    z = ctx.synthetic_witness(n, 0x5EED0002)
+    t = time.perf_counter()
+    crs = zkp.CRS.generate_from_qap(ctx, qap, zkp.SetupParams(*params), 1)   # host key for the checker
+    opk = bench.oracle_pk(oracle, crs.pk)
+    del crs
+    zh = z.cpu().numpy().view(np.uint64)
+    rc, oproof = oracle.prove(opk, oracle.CSR.synthetic(n), zh, 1, r, s)
+    del opk
+    assert rc == 0
+    print(f"\n[2^24] oracle proof on {oracle.default_threads()} threads: {time.perf_counter() - t:.1f} s", flush=True)
+    assert oracle.proof_compress(oproof).hex() == ORACLE_2P24
+    return qap, params, r, s, z, oproof
+
+
+@pytest.mark.timeout(900)
+def test_2p24_single_gpu_prove(ctx, zkp, case_2p24):
+    qap, params, r, s, z, oproof = case_2p24
+    n = 1 << LOG_N
+    t = time.perf_counter()
+    dpk = zkp.CRS.generate_device(ctx, qap, zkp.SetupParams(*params), 1)
+    t_setup = time.perf_counter() - t
+    try:
+        zkp.Prover.prove_device(dpk, z.data_ptr(), 3 * n + 1, 1, r, s)
+        t = time.perf_counter()
+        proof = zkp.Prover.prove_device(dpk, z.data_ptr(), 3 * n + 1, 1, r, s)
+        dt = time.perf_counter() - t
+    finally:
+        dpk.free()
+    print(f"[2^24] GPU setup {t_setup:.2f} s, prove {dt * 1e3:.1f} ms; build {zkp.build_id()}", flush=True)
+    assert np.array_equal(proof.words, oproof)
+
+
+@pytest.mark.timeout(900)
+def test_2p24_eight_shards_virtual_and_partial(ctx, zkp, case_2p24):
+    qap, params, r, s, z, oproof = case_2p24
+    n, N = 1 << LOG_N, 8
+    t = time.perf_counter()
+    dpks = [zkp.CRS.generate_device(ctx, qap, zkp.SetupParams(*params), 1, shard=k, nshards=N) for k in range(N)]
+    t_setup = time.perf_counter() - t
+    try:
+        t = time.perf_counter()
+        proof_v = zkp.Prover.prove_virtual_shards(dpks, z.data_ptr(), 3 * n + 1, 1, r, s)
+        t_v = time.perf_counter() - t
+        assert np.array_equal(proof_v.words, oproof), "8 virtual shards (distributed quotient)"
+        t = time.perf_counter()
+        parts = [zkp.Prover.prove_partial(d, z.data_ptr(), 3 * n + 1, 1, r, s) for d in dpks]
+        t_p = time.perf_counter() - t
+        proof_p = zkp.Prover.combine(parts, r, s)
+        assert np.array_equal(proof_p.words, oproof), "8 shards' prove_partial + combine"
+    finally:
+        for d in dpks:
+            d.free()
+    print(f"[2^24 x 8 shards] GPU setup {t_setup:.2f} s, virtual-rank proof {t_v * 1e3:.0f} ms, "
+          f"8 partials (replicated quotient) {t_p * 1e3:.0f} ms", flush=True)

@@ -173,8 +173,8 @@ def test_msm_rejects_bad_scalars(ctx, zkp, oracle):
 
 @pytest.mark.parametrize("log_n", [10, 13])
 def test_schedules_give_the_same_proof(ctx, zkp, oracle, log_n):
-    """zk_ctx_set_schedule (overlapped, G2-after-quotient, serial, quotient
-    first) changes only the stream order: the oracle's proof every time."""
+    """zk_ctx_set_schedule (overlapped, serial) changes only the stream
+    order: the oracle's proof every time."""
     import torch
     n = 1 << log_n
     qap = zkp.QAP(zkp.CSRMatrices.synthetic(n))
@@ -188,7 +188,7 @@ def test_schedules_give_the_same_proof(ctx, zkp, oracle, log_n):
     assert rc == 0
     dpk = zkp.CRS.generate_device(ctx, qap, zkp.SetupParams(*params), 1)
     try:
-        for sched in (0, 1, 3, 4, 5, 6, 7, 8, 9, -1):
+        for sched in (0, 3, -1):
             ctx.set_schedule(sched)
             p = zkp.Prover.prove_device(dpk, z.data_ptr(), len(zh), 1, r, s)
             torch.cuda.synchronize()

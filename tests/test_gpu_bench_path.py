@@ -1,9 +1,12 @@
 """bench.py's N > 1 path (the configs[4] strong-scaling line) rehearsed on ONE
 GPU: two torchrun ranks on device 0 with gloo collectives
-(ZK_BENCH_DIST_BACKEND=gloo ZK_BENCH_DEVICE=0; no RCCL communicator, so each
-rank recomputes the quotient -- the line says "quotient": "replicated").  The
+(ZK_BENCH_DIST_BACKEND=gloo ZK_BENCH_DEVICE=0).  RCCL refuses two ranks on
+one device, so the distributed quotient's three all-to-alls run through the
+library's host-staged exchange over the gloo group ("quotient":
+"distributed-host") -- the same stages and index maps as over RCCL.  The
 folded proof of the sharded run must equal the single-GPU proof of the same
-circuit, key parameters, witness and r, s byte for byte."""
+circuit, key parameters, witness and r, s byte for byte, and the
+PCIe-inclusive leg must send each rank only its ~1/N witness slice."""
 import json
 import os
 import socket
@@ -37,7 +40,9 @@ def test_bench_two_rank_path_matches_single_gpu(ctx, zkp):
     line = [ln for ln in res.stdout.splitlines() if ln.startswith("{")][-1]
     rec = json.loads(line)
     assert rec["n_gpus"] == 2 and rec["scaling"] == "strong"
-    assert rec["config"]["constraints"] == 1 << log_n and rec["config"]["quotient"] == "replicated"
+    assert rec["config"]["constraints"] == 1 << log_n and rec["config"]["quotient"] == "distributed-host"
+    pc = rec["pcie_inclusive"]
+    assert pc["max_rank_witness_bytes"] <= pc["witness_bytes"] // 2 + 64
     sys.path.insert(0, ROOT)
     import bench
     params, r, s = bench.setup_params(seed)

@@ -1,0 +1,136 @@
+"""The distributed quotient across REAL processes, without RCCL: N ranks on
+one GPU, each with its own zk_ctx and key shard, the three all-to-alls of
+dist.hip going through the library's host-staged exchange
+(zk_ctx_attach_exchange) over a torch.distributed gloo group.  RCCL refuses
+two ranks on one device, so this is the multi-process rehearsal of the path
+the 8-GPU run takes (only ncclAllToAll itself differs).
+
+  * every rank proves from its HOST witness slice only
+    (zk_groth16_witness_ranges / zk_groth16_prove_partial_host: ~1/N of z,
+    the MSM bases being sharded by quotient-row ownership), the partials meet
+    in one all-gather and the folded proof equals the C oracle's;
+  * the device-witness partial (zk_groth16_prove_partial) equals the
+    host-slice one byte for byte;
+  * a rank that fails mid-quotient (ZK_OPT_FAULT_AFTER_EXCHANGE: right after
+    the 2nd all-to-all) aborts the exchange: it returns its error, its peer
+    -- blocked in the 3rd all-to-all -- returns ZK_ERR_RCCL instead of
+    hanging, and the aborted exchange refuses further proofs."""
+import json
+import os
+import socket
+import time
+from datetime import timedelta
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _worker(rank, world, port, log_n, seed, out_dir, fault):
+    import importlib
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    import binding as oracle   # checker data only: the witness generator
+    import pyref
+    zkp = importlib.import_module("zero-knowledge-proofs_amd")
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=30))
+    res = {"rank": rank}
+    n = 1 << log_n
+    rng = pyref.SplitMix64(seed)
+    params = [rng.fr() for _ in range(5)]
+    r, s = rng.fr(), rng.fr()
+    ctx = zkp.Context(0)
+    ctx.attach_exchange(zkp.TorchExchange(), rank, world)
+    qap = zkp.QAP(zkp.CSRMatrices.synthetic(n))
+    dpk = zkp.CRS.generate_device(ctx, qap, zkp.SetupParams(*params), 1, shard=rank, nshards=world)
+    z = oracle.synthetic_witness(n, seed + 1)
+    ranges = dpk.witness_ranges()
+    zs = dpk.witness_slice(z)
+    res["slice_rows"], res["zlen"] = int(len(zs)), int(len(z))
+    res["ranges"] = int(len(ranges))
+    part = zkp.Prover.prove_partial_host(dpk, zs, len(z), 1, r, s)
+    dz = torch.from_numpy(z.view(np.int64).copy()).cuda()
+    part_dev = zkp.Prover.prove_partial(dpk, dz.data_ptr(), len(z), 1, r, s)
+    res["device_partial_equal"] = part_dev == part
+    parts = [None] * world
+    dist.all_gather_object(parts, part)
+    if rank == 0:
+        res["proof"] = [int(w) for w in zkp.Prover.combine(parts, r, s).words]
+    if fault:
+        if rank == 1:
+            ctx.set_option(zkp.ZK_OPT_FAULT_AFTER_EXCHANGE, 2)
+        t = time.perf_counter()
+        try:
+            zkp.Prover.prove_partial_host(dpk, zs, len(z), 1, r, s)
+            res["fault_error"] = None
+        except Exception as e:   # noqa: BLE001 -- the kind is the result
+            res["fault_error"] = type(e).__name__
+        res["fault_s"] = time.perf_counter() - t
+        try:
+            zkp.Prover.prove_partial_host(dpk, zs, len(z), 1, r, s)
+            res["after_abort_error"] = None
+        except Exception as e:   # noqa: BLE001
+            res["after_abort_error"] = type(e).__name__
+    with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
+        json.dump(res, f)
+    dpk.free()
+    ctx.close()
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def _run(tmp_path, world, log_n, seed, fault):
+    mp.spawn(_worker, args=(world, _free_port(), log_n, seed, str(tmp_path), fault), nprocs=world, join=True)
+    return [json.load(open(tmp_path / f"rank{k}.json")) for k in range(world)]
+
+
+def _oracle_proof(oracle, log_n, seed):
+    import pyref
+    n = 1 << log_n
+    rng = pyref.SplitMix64(seed)
+    params = [rng.fr() for _ in range(5)]
+    r, s = rng.fr(), rng.fr()
+    csr = oracle.CSR.synthetic(n)
+    rc, opk, _ = oracle.setup(csr, params, 1, nthreads=8)
+    assert rc == 0
+    rc, proof = oracle.prove(opk, csr, oracle.synthetic_witness(n, seed + 1), 1, r, s)
+    assert rc == 0
+    return [int(w) for w in proof]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4])
+def test_host_exchange_sliced_witness_matches_oracle(oracle, tmp_path, world):
+    log_n, seed = 10, 31337 + world
+    res = _run(tmp_path, world, log_n, seed, False)
+    assert res[0]["proof"] == _oracle_proof(oracle, log_n, seed)
+    for r in res:
+        assert r["device_partial_equal"]
+        # z_0 plus this rank's rows' variables: ~1/N of the witness
+        assert r["slice_rows"] <= r["zlen"] // world + 2, r
+
+
+@pytest.mark.timeout(300)
+def test_rank_failure_mid_quotient_aborts_peers(oracle, tmp_path):
+    log_n, seed = 10, 4711
+    res = _run(tmp_path, 2, log_n, seed, True)
+    assert res[0]["proof"] == _oracle_proof(oracle, log_n, seed)
+    assert res[1]["fault_error"] == "DeviceError"        # the injected rank-local failure
+    assert res[0]["fault_error"] == "ExchangeError"      # the peer: ZK_ERR_RCCL, not a hang
+    assert res[0]["fault_s"] < 45 and res[1]["fault_s"] < 45
+    for r in res:
+        assert r["after_abort_error"] == "ExchangeError"

@@ -54,3 +54,27 @@ def test_ntt_roundtrip_large(ctx, oracle, log_n):
     # X_0 = sum_j x_j
     R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
     assert oracle.fr_ints(y[:1])[0] == sum(oracle.fr_ints(x)) % R
+
+
+@pytest.mark.parametrize("log_n", [0, 1, 10, 13])
+@pytest.mark.parametrize("where", ["first", "last"])
+def test_ntt_rejects_non_canonical_input(ctx, zkp, oracle, log_n, where):
+    """An element >= r (here = r, and all-ones limbs) is ZK_ERR_ARG on both
+    entry points -- checked in the first pass's load -- like every other
+    Fr input of the ABI; a valid transform after it still matches."""
+    import ctypes as C
+    import torch
+    R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    n = 1 << log_n
+    for bad in ([(R >> (64 * i)) & (2 ** 64 - 1) for i in range(4)], [2 ** 64 - 1] * 4):
+        x = oracle.random_fr(n, 5 + log_n)
+        x[0 if where == "first" else n - 1] = bad
+        for inverse in (False, True):
+            with pytest.raises(ValueError):
+                ctx.ntt(x, inverse=inverse)
+        d = torch.from_numpy(x.view(np.int64).copy()).cuda()
+        rc = zkp.lib().zk_ntt_fr_dev(C.c_void_p(ctx._h), C.c_void_p(d.data_ptr()), C.c_uint32(log_n), C.c_int(1),
+                                    None)
+        assert rc == zkp.ZK_ERR_ARG
+    x = oracle.random_fr(n, 6 + log_n)
+    assert np.array_equal(ctx.ntt(x), oracle.fft(x))

@@ -1,83 +1,69 @@
-"""Non-default prover paths stay bit-exact, each in a child process (the
-switches are read once per process).  The unfused quotient path (ZK_NTT_FUSE=0: iNTT, separate n^-1 g^i scale,
-NTT) stays bit-exact: it is the fallback the fused tile kernel replaced and
-no other test runs it (the switch is read once per process, so a child
-process runs it).  Sizes cover 1 NTT pass (2^0 .. 2^11), 2 passes (2^12) and
-3 passes (2^21)."""
-import os
-import subprocess
-import sys
+"""The prover paths the library picks by size, each forced at small sizes
+through zk_ctx_set_option (explicit ctx options; the library reads no
+environment variables) and checked bit for bit against the C oracle:
 
+  ZK_OPT_QUOTIENT_PATH = 1  the large-domain quotient (separate iNTT /
+                            bit-reversed-table coset scale / NTT passes, and
+                            the final coset iNTT in natural order through
+                            ntt_natural) that the library takes from 2^23
+                            constraints, at 1-, 2- and 3-pass sizes
+                            including the size-1 domain;
+  ZK_OPT_PROVE_WIN_C = 22   the 3-window / 2^21-bucket prove plan taken from
+                            2^24 constraints per key shard (the batch keys
+                            reach 23 bits, so the radix sort, merge and
+                            bucket reduction see 2^21-bucket segments).
+The defaults themselves run at 2^24 in tests/test_gpu_2p24.py."""
+import numpy as np
 import pytest
 
+import gpu_util as U
+
 pytestmark = pytest.mark.gpu
-HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-@pytest.mark.timeout(300)
-def test_unfused_quotient_matches_oracle():
-    env = dict(os.environ, ZK_NTT_FUSE="0")
-    res = subprocess.run([sys.executable, os.path.join(HERE, "unfused_quotient_check.py"), "ZK_NTT_FUSE=0", "0", "1", "11",
-                          "12", "21"],
-                         env=env, capture_output=True, text=True, timeout=280)
-    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
-    assert res.stdout.count(" ok") == 5
+def _prove_vs_oracle(ctx, zkp, oracle, log_n):
+    import pyref
+    n = 1 << log_n
+    rng = pyref.SplitMix64(900 + log_n)
+    params = [rng.fr() for _ in range(5)]
+    r, s = rng.fr(), rng.fr()
+    qap = zkp.QAP(zkp.CSRMatrices.synthetic(n))
+    crs = zkp.CRS.generate_from_qap(ctx, qap, zkp.SetupParams(*params), 1)
+    z = oracle.synthetic_witness(n, 901 + log_n)
+    rc, want = oracle.prove(U.oracle_pk_from(oracle, crs.pk), oracle.CSR.synthetic(n), z, 1, r, s)
+    assert rc == 0
+    dpk = crs.pk.upload(ctx)
+    got = zkp.Prover.prove(dpk, zkp.Witness(z, 1), r=r, s=s)
+    dpk.free()
+    assert np.array_equal(got.words, want), f"2^{log_n}"
 
 
-@pytest.mark.timeout(300)
-def test_large_domain_quotient_path_matches_oracle():
-    """ZK_NTT_FUSE=0 ZK_H_NATURAL=1: the quotient path the library picks from
-    2^23 constraints up (separate iNTT / bit-reversed-table coset scale / NTT,
-    and the final coset iNTT in natural order through ntt_natural), forced
-    at 1-, 2- and 3-pass sizes including the size-1 domain."""
-    env = dict(os.environ, ZK_NTT_FUSE="0", ZK_H_NATURAL="1")
-    res = subprocess.run([sys.executable, os.path.join(HERE, "unfused_quotient_check.py"), "ZK_H_NATURAL=1", "0", "1",
-                          "11", "12", "21"], env=env, capture_output=True, text=True, timeout=280)
-    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
-    assert res.stdout.count(" ok") == 5
+@pytest.mark.parametrize("log_n", [0, 1, 11, 12, 21])
+def test_large_domain_quotient_path_matches_oracle(zkp, oracle, log_n):
+    with zkp.Context(0) as ctx:
+        ctx.set_option(zkp.ZK_OPT_QUOTIENT_PATH, 1)
+        _prove_vs_oracle(ctx, zkp, oracle, log_n)
 
 
-@pytest.mark.timeout(300)
-def test_natural_final_with_fused_shift_matches_oracle():
-    """ZK_H_NATURAL=1 with the fused coset shift (the two switches combine)."""
-    env = dict(os.environ, ZK_H_NATURAL="1")
-    res = subprocess.run([sys.executable, os.path.join(HERE, "unfused_quotient_check.py"), "ZK_H_NATURAL=1", "2",
-                          "13"], env=env, capture_output=True, text=True, timeout=280)
-    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
-    assert res.stdout.count(" ok") == 2
+@pytest.mark.parametrize("log_n", [0, 13])
+def test_small_domain_quotient_path_forced_matches_oracle(zkp, oracle, log_n):
+    with zkp.Context(0) as ctx:
+        ctx.set_option(zkp.ZK_OPT_QUOTIENT_PATH, 0)
+        _prove_vs_oracle(ctx, zkp, oracle, log_n)
 
 
-@pytest.mark.timeout(300)
-def test_lazy_accumulate_matches_oracle():
-    """ZK_LAZY_ACCUM=1: the G1 bucket accumulate in csrc/lazy.hpp's redundant
-    signed-limb Fq form (an opt-in experiment) against the oracle."""
-    env = dict(os.environ, ZK_LAZY_ACCUM="1")
-    res = subprocess.run([sys.executable, os.path.join(HERE, "unfused_quotient_check.py"), "ZK_LAZY_ACCUM=1", "2", "10",
-                          "16"], env=env, capture_output=True, text=True, timeout=280)
-    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
-    assert res.stdout.count(" ok") == 3
+@pytest.mark.parametrize("log_n", [4, 12])
+def test_three_window_plan_matches_oracle(zkp, oracle, log_n):
+    with zkp.Context(0) as ctx:
+        ctx.set_option(zkp.ZK_OPT_PROVE_WIN_C, 22)
+        _prove_vs_oracle(ctx, zkp, oracle, log_n)
 
 
-@pytest.mark.timeout(300)
-def test_packed_bases_match_oracle():
-    """ZK_BASE_PAD=0: the proving key's window copies stay packed (96-byte G1,
-    192-byte G2 points) instead of line-padded -- the accumulate's base
-    stride is a launch parameter, so both layouts must prove the same bytes."""
-    env = dict(os.environ, ZK_BASE_PAD="0")
-    res = subprocess.run([sys.executable, os.path.join(HERE, "unfused_quotient_check.py"), "ZK_BASE_PAD=0", "3", "10",
-                          "14"], env=env, capture_output=True, text=True, timeout=280)
-    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
-    assert res.stdout.count(" ok") == 3
-
-
-@pytest.mark.timeout(300)
-def test_three_window_plan_matches_oracle():
-    """ZK_PROVE_WIN_C=22: the 3-window / 2^21-bucket plan the library picks
-    from 2^24 constraints up, forced at small sizes (the batch keys reach
-    23 bits, so the radix sort, merge and bucket reduction see 2^21-bucket
-    segments)."""
-    env = dict(os.environ, ZK_PROVE_WIN_C="22")
-    res = subprocess.run([sys.executable, os.path.join(HERE, "unfused_quotient_check.py"), "ZK_PROVE_WIN_C=22", "4",
-                          "12"], env=env, capture_output=True, text=True, timeout=280)
-    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
-    assert res.stdout.count(" ok") == 2
+def test_options_reject_unknown_values(zkp):
+    with zkp.Context(0) as ctx:
+        for opt, val in ((zkp.ZK_OPT_QUOTIENT_PATH, 2), (zkp.ZK_OPT_PROVE_WIN_C, 17), (99, 0)):
+            with pytest.raises(ValueError):
+                ctx.set_option(opt, val)
+        for sched in (1, 4, 9):
+            with pytest.raises(ValueError):
+                ctx.set_schedule(sched)

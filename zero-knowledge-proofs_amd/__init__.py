@@ -23,7 +23,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# ZK_AMD_LIB: an alternative build of the same library (tuning A/B runs)
+# ZK_AMD_LIB: an alternative build of the same library (tooling: A/B runs of
+# variant builds; the library itself reads no environment variables)
 LIB_PATH = os.environ.get("ZK_AMD_LIB") or os.path.join(_HERE, "libzkp_amd.so")
 
 R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001  # Fr modulus
@@ -46,8 +47,10 @@ EXPORTS = (
     "zk_test_prove_virtual_shards", "zk_proof_deserialize_compressed", "zk_groth16_verify",
     "zk_groth16_verify_batch", "zk_pairing_product_is_one", "zk_msm_g1_upload_windows",
     "zk_msm_g2_upload_windows", "zk_build_id", "zk_ctx_set_schedule", "zk_qap_evaluate_at",
-    "zk_poly_evaluate_batch", "zk_synthetic_witness_dev",
+    "zk_poly_evaluate_batch", "zk_synthetic_witness_dev", "zk_ctx_set_option", "zk_ctx_timeline_read",
+    "zk_ctx_attach_exchange", "zk_groth16_witness_ranges", "zk_groth16_prove_partial_host",
 )
+ZK_OPT_QUOTIENT_PATH, ZK_OPT_PROVE_WIN_C, ZK_OPT_EXCHANGE_TIMEOUT_MS, ZK_OPT_FAULT_AFTER_EXCHANGE = 1, 2, 3, 4
 CSRC = os.path.join(_HERE, "csrc")
 
 
@@ -88,13 +91,26 @@ class DeviceError(GrothError):
     pass
 
 
+class ExchangeError(DeviceError):
+    """ZK_ERR_RCCL: the multi-GPU exchange (RCCL or host-staged) failed or was aborted."""
+
+
 _STATUS = {ZK_ERR_MSM_LEN: MSMError, ZK_ERR_INVALID_WITNESS: InvalidWitness,
            ZK_ERR_QAP_DIVISION: PolynomialDivisionFailed, ZK_ERR_DOMAIN: DomainTooSmall,
            ZK_ERR_SETUP_PARAMS: SetupError, ZK_ERR_DEVICE: DeviceError,
-           ZK_ERR_RCCL: DeviceError, ZK_ERR_ARG: ValueError, ZK_ERR_DIMENSION: DimensionMismatch}
+           ZK_ERR_RCCL: ExchangeError, ZK_ERR_ARG: ValueError, ZK_ERR_DIMENSION: DimensionMismatch}
 
 
 # ---------------------------------------------------------- C structs ----
+_A2A_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
+_AMAX_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p)
+_ABORT_FN = C.CFUNCTYPE(None, C.c_void_p)
+
+
+class _ExchangeOps(C.Structure):
+    _fields_ = [("all_to_all", _A2A_FN), ("all_reduce_max", _AMAX_FN), ("abort", _ABORT_FN), ("user", C.c_void_p)]
+
+
 class _Fr(C.Structure):
     _fields_ = [("l", C.c_uint64 * 4)]
 
@@ -275,10 +291,56 @@ class Context:
         _check(lib().zk_ctx_attach_rccl(C.c_void_p(self._h), buf, C.c_int(rank), C.c_int(world)), self,
                "zk_ctx_attach_rccl")
 
+    def attach_exchange(self, exchange, rank, world):
+        """zk_ctx_attach_exchange: the distributed quotient of sharded keys
+        over a host-staged transport.  `exchange` has all_to_all(send_ptr,
+        recv_ptr, chunk_bytes), all_reduce_max(int) -> int and abort()
+        (e.g. TorchExchange over a gloo process group)."""
+        def a2a(_u, send, recv, chunk):
+            try:
+                exchange.all_to_all(send, recv, chunk)
+                return 0
+            except Exception:
+                return 1
+
+        def amax(_u, pv):
+            try:
+                p = C.cast(pv, C.POINTER(C.c_int32))
+                p[0] = int(exchange.all_reduce_max(int(p[0])))
+                return 0
+            except Exception:
+                return 1
+
+        def abort(_u):
+            try:
+                exchange.abort()
+            except Exception:
+                pass
+        ops = _ExchangeOps(_A2A_FN(a2a), _AMAX_FN(amax), _ABORT_FN(abort), None)
+        self._exchange_refs = (ops, exchange)   # the callbacks must outlive the attachment
+        _check(lib().zk_ctx_attach_exchange(C.c_void_p(self._h), C.byref(ops), C.c_int(rank), C.c_int(world)), self,
+               "zk_ctx_attach_exchange")
+
     def set_schedule(self, schedule=-1):
-        """zk_ctx_set_schedule: -1 default, 0 overlapped streams, 3 every prove
-        kernel in order on one stream (isolated kernel durations)."""
+        """zk_ctx_set_schedule: -1 / 0 overlapped streams (default), 3 every
+        prove kernel in order on one stream (isolated kernel durations)."""
         _check(lib().zk_ctx_set_schedule(C.c_void_p(self._h), C.c_int(int(schedule))), self, "zk_ctx_set_schedule")
+
+    def set_option(self, option, value):
+        """zk_ctx_set_option: ZK_OPT_QUOTIENT_PATH (-1 by size, 0 small-domain,
+        1 large-domain) or ZK_OPT_PROVE_WIN_C (0 by size, 16, 22; keys made
+        afterwards).  Explicit path choices for tests and A/B runs."""
+        _check(lib().zk_ctx_set_option(C.c_void_p(self._h), C.c_int(int(option)), C.c_int64(int(value))), self,
+               "zk_ctx_set_option")
+
+    def timeline_read(self):
+        """The per-launch stream timeline recorded under profile(2), as text."""
+        n = C.c_size_t()
+        _check(lib().zk_ctx_timeline_read(C.c_void_p(self._h), None, C.c_size_t(0), C.byref(n)), self, "timeline")
+        buf = C.create_string_buffer(n.value + 1)
+        _check(lib().zk_ctx_timeline_read(C.c_void_p(self._h), buf, C.c_size_t(n.value + 1), C.byref(n)), self,
+               "timeline")
+        return buf.value.decode()
 
     def synthetic_witness(self, n, seed):
         """The groth16-cli circuit's witness z (3n+1 canonical Fr) generated
@@ -291,6 +353,7 @@ class Context:
 
     # ---- live kernel timing (HIP events on the launching stream) ----
     def profile(self, enable=True):
+        """0/False off, 1/True per-phase kernel times, 2 also the stream timeline."""
         _check(lib().zk_ctx_profile(C.c_void_p(self._h), C.c_int(int(enable))), self, "zk_ctx_profile")
 
     def profile_read(self):
@@ -637,6 +700,24 @@ class DeviceProvingKey:
         _check(rc, ctx, "zk_pk_upload")
         return cls(ctx, h.value, pk.qap)
 
+    def witness_ranges(self):
+        """zk_groth16_witness_ranges: (k, 2) array of the [lo, hi) witness
+        index ranges this shard reads on its ctx."""
+        n = C.c_size_t()
+        _check(lib().zk_groth16_witness_ranges(C.c_void_p(self.ctx._h), C.c_void_p(self._h), None, C.c_size_t(0),
+                                               C.byref(n)), self.ctx, "zk_groth16_witness_ranges")
+        out = np.zeros((max(n.value, 1), 2), dtype=np.uint64)
+        _check(lib().zk_groth16_witness_ranges(C.c_void_p(self.ctx._h), C.c_void_p(self._h), _p(out),
+                                               C.c_size_t(n.value), C.byref(n)), self.ctx, "zk_groth16_witness_ranges")
+        return out[:n.value]
+
+    def witness_slice(self, assignment):
+        """This shard's part of a full witness (rows of every witness range, in order)."""
+        a = np.asarray(assignment, dtype=np.uint64).reshape(-1, 4)
+        rs = self.witness_ranges()
+        return np.ascontiguousarray(np.concatenate([a[int(lo):int(hi)] for lo, hi in rs]) if len(rs)
+                                    else np.zeros((0, 4), dtype=np.uint64))
+
     def free(self):
         if getattr(self, "_h", None):
             lib().zk_pk_free(C.c_void_p(self._h))
@@ -811,6 +892,20 @@ class Prover:
         return bytes(buf)
 
     @staticmethod
+    def prove_partial_host(dpk, z_slice, zlen, num_public, r, s):
+        """This GPU's shard of the proof from a HOST witness slice (only the
+        entries of dpk.witness_ranges(), concatenated: dpk.witness_slice(z));
+        zlen = length of the whole witness."""
+        ctx = dpk.ctx
+        zs = np.ascontiguousarray(z_slice, dtype=np.uint64).reshape(-1, 4)
+        buf = (C.c_uint8 * PARTIAL_BYTES)()
+        rc = lib().zk_groth16_prove_partial_host(C.c_void_p(ctx._h), C.c_void_p(dpk._h), _p(zs) if len(zs) else None,
+                                                 C.c_size_t(len(zs)), C.c_size_t(zlen), C.c_size_t(num_public),
+                                                 C.byref(_fr(r)), C.byref(_fr(s)), buf)
+        _check(rc, ctx, "zk_groth16_prove_partial_host")
+        return bytes(buf)
+
+    @staticmethod
     def prove_virtual_shards(dpks, d_z_ptr, zlen, num_public, r, s):
         """Diagnostic: the distributed quotient + sharded MSMs of len(dpks)
         virtual ranks on one device (zk_test_prove_virtual_shards)."""
@@ -832,6 +927,36 @@ class Prover:
                                             C.byref(out))
         _check(rc, None, "zk_groth16_prove_combine")
         return Proof._from_c(out)
+
+
+class TorchExchange:
+    """Host-staged exchange over a torch.distributed process group (CPU
+    tensors: gloo), for Context.attach_exchange: the distributed quotient's
+    three all-to-alls as all_to_all_single, the status agreement as a MAX
+    all-reduce.  abort() tears the group down (the default group unless one
+    is given), so peers blocked in a transfer with this rank fail instead of
+    waiting out the group's timeout."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist, self.group = dist, group
+
+    def all_to_all(self, send_ptr, recv_ptr, chunk_bytes):
+        import torch
+        nbytes = chunk_bytes * self.dist.get_world_size(self.group)
+        send = torch.frombuffer((C.c_uint8 * nbytes).from_address(send_ptr), dtype=torch.uint8)
+        recv = torch.frombuffer((C.c_uint8 * nbytes).from_address(recv_ptr), dtype=torch.uint8)
+        self.dist.all_to_all_single(recv, send, group=self.group)
+
+    def all_reduce_max(self, value):
+        import torch
+        t = torch.tensor([value], dtype=torch.int64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        return int(t.item())
+
+    def abort(self):
+        if self.dist.is_initialized():
+            self.dist.destroy_process_group(self.group)
 
 
 # ------------------------------------------------------------- verify ----

@@ -12,6 +12,9 @@ int prove_virtual_shards_impl(zk_ctx*, const zk_pk_dev* const*, uint32_t, const 
                               const zk_fr*, const zk_fr*, zk_proof*);
 int prove_partial_impl(zk_ctx*, const zk_pk_dev*, const void*, size_t, size_t, const zk_fr*, const zk_fr*,
                        zk_prove_partial*);
+int prove_partial_host_impl(zk_ctx*, const zk_pk_dev*, const zk_fr*, size_t, size_t, size_t, const zk_fr*,
+                            const zk_fr*, zk_prove_partial*);
+std::vector<uint64_t> witness_ranges(const zk_ctx*, const zk_pk_dev*);
 int combine_impl(const zk_prove_partial*, size_t, const zk_fr*, const zk_fr*, zk_proof*);
 int setup_impl(zk_ctx*, const zk_r1cs_csr*, const zk_setup_params*, uint64_t, uint32_t, uint32_t, zk_pk*,
                zk_pk_dev**, zk_vk*);
@@ -56,21 +59,12 @@ zk_ctx* zk_ctx_create(int device) {
     int lo_prio = 0, hi_prio = 0;
     ZK_HIP(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
     ZK_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio));   // quotient + H
-    // side[0]: G2 MSM (high), side[1..]: the G1 groups (low).  Tuning:
-    // ZK_G2_PRIO=lo puts the G2 stream low; ZK_SIDE_PRIO lists h/l per side
-    // stream (e.g. "hhl") and overrides both.
-    const char* g2p = getenv("ZK_G2_PRIO");
-    const char* sp = getenv("ZK_SIDE_PRIO");
-    for (int i = 0; i < NUM_SIDE; i++) {
-      bool hi = i == 0 ? !(g2p && g2p[0] == 'l') : false;
-      if (sp && (int)std::strlen(sp) > i) hi = sp[i] == 'h';
-      ZK_HIP(hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking, hi ? hi_prio : lo_prio));
-    }
-    ZK_HIP(hipEventCreateWithFlags(&c->ev_quot, hipEventDisableTiming));
+    // side[0]: G2 MSM (high), side[1..]: the G1 batches (low); other
+    // priority assignments measured within noise
+    for (int i = 0; i < NUM_SIDE; i++)
+      ZK_HIP(hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking, i == 0 ? hi_prio : lo_prio));
     ZK_HIP(hipEventCreateWithFlags(&c->ev_scal, hipEventDisableTiming));
-    ZK_HIP(hipEventCreateWithFlags(&c->ev_hsort, hipEventDisableTiming));
     for (auto& e : c->ev_done) ZK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    for (auto& e : c->ev_acc) ZK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     return c.release();
   } catch (...) {
     return nullptr;
@@ -85,11 +79,8 @@ void zk_ctx_destroy(zk_ctx* ctx) {
   ctx->domains.clear();
   for (int i = 0; i < NUM_SIDE; i++) (void)hipStreamDestroy(ctx->side[i]);
   (void)hipStreamDestroy(ctx->stream);
-  (void)hipEventDestroy(ctx->ev_quot);
   (void)hipEventDestroy(ctx->ev_scal);
-  (void)hipEventDestroy(ctx->ev_hsort);
   for (auto& e : ctx->ev_done) (void)hipEventDestroy(e);
-  for (auto& e : ctx->ev_acc) (void)hipEventDestroy(e);
   delete ctx;
 }
 
@@ -97,8 +88,26 @@ const char* zk_last_error(const zk_ctx* ctx) { return ctx ? ctx->err.c_str() : "
 
 int zk_ctx_profile(zk_ctx* ctx, int enable) {
   if (!ctx) return ZK_ERR_ARG;
+  if (enable < 0 || enable > 2) return ZK_ERR_ARG;
   ctx->prof.on = enable != 0;
-  if (!enable) ctx->prof.stats.clear();
+  ctx->prof.timeline = enable == 2;
+  if (!enable) {
+    ctx->prof.stats.clear();
+    ctx->prof.tl.clear();
+  }
+  return ZK_OK;
+}
+
+int zk_ctx_timeline_read(zk_ctx* ctx, char* buf, size_t cap, size_t* len) {
+  if (!ctx || !len) return ZK_ERR_ARG;
+  const std::string& t = ctx->prof.tl;
+  *len = t.size();
+  if (buf && cap) {
+    const size_t k = std::min(cap - 1, t.size());
+    std::memcpy(buf, t.data(), k);
+    buf[k] = 0;
+    if (k == t.size()) ctx->prof.tl.clear();
+  }
   return ZK_OK;
 }
 
@@ -221,17 +230,8 @@ int zk_msm_g2(zk_ctx* ctx, const zk_g2_affine* bases, size_t nb, const zk_fr* sc
 // Window width c: 16 up to 64-bit scalars (4 windows, 2^15 buckets), 20 for
 // wider ones -- 13 windows over 2^19 buckets instead of 16 over 2^15: the
 // 2^20 full-width MSM 3.79-3.87 vs 3.92-4.01 ms; c = 18, 19, 22 lose
-// (4.5-5.0 ms; profiles/r02_upload_win_sweep.txt).  ZK_UPLOAD_WIN_C
-// overrides (8..22).
-static int upload_win_c(uint32_t win_bits) {
-  static const int env = [] {
-    const char* e = getenv("ZK_UPLOAD_WIN_C");
-    const int v = e ? atoi(e) : 0;
-    return v >= 8 && v <= 22 ? v : 0;
-  }();
-  if (env) return env;
-  return win_bits > 64 ? 20 : 16;
-}
+// (4.5-5.0 ms; profiles/r02_upload_win_sweep.txt).
+static int upload_win_c(uint32_t win_bits) { return win_bits > 64 ? 20 : 16; }
 
 template <class C, class ABI>
 static int msm_upload(zk_ctx* ctx, const ABI* bases, size_t n, int group, uint32_t win_bits, zk_msm_bases** out) {
@@ -348,14 +348,32 @@ int zk_msm_g2_dev(zk_ctx* ctx, const zk_msm_bases* b, const void* d_sc, size_t n
 // The transform runs on the canonical values as they are: with twiddles in
 // Montgomery form w R, a butterfly's fp_mul(v, w R) = v w, so canonical data
 // stay canonical through every pass and no to/from-Montgomery pass is needed.
-// Forward: DIF (its first pass reads d_data, scaled by g^i for a coset, into
-// the scratch) then the tiled bit reversal back into d_data; inverse: DIF
-// with the inverse twiddles, the bit reversal applying n^-1 (coset: n^-1 g^-i).
+// Natural order in and out (ntt_natural: DIT passes, the first gathering its
+// tile from the bit-reversed positions).  Every input element is checked to
+// be a canonical Fr (ark's Fr is always reduced) in that first pass's load:
+// a flag, read after the transform, turns into ZK_ERR_ARG (the data are then
+// unspecified).  The caller synchronises.
 static int ntt_device(zk_ctx* ctx, void* d_data, uint32_t log_n, int dir, const zk_fr* coset) {
   hipStream_t st = ctx->stream;
   const size_t n = (size_t)1 << log_n;
   if (coset && !fr_canonical(*coset)) return ZK_ERR_ARG;
-  if (log_n == 0) return ZK_OK;   // a size-1 DFT (and its coset / inverse) is the identity
+  ctx->flags.ensure(16);
+  ctx->flags_host.ensure(16);
+  ZK_HIP(hipMemsetAsync(ctx->flags.p, 0, 4, st));
+  uint32_t* chk = ctx->flags.as<uint32_t>();
+  auto flag_result = [&]() {
+    ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
+    ZK_HIP(hipStreamSynchronize(st));
+    if (*ctx->flags_host.as<uint32_t>()) {
+      ctx->err = "an NTT input element is not a canonical Fr (>= r)";
+      return (int)ZK_ERR_ARG;
+    }
+    return (int)ZK_OK;
+  };
+  if (log_n == 0) {   // a size-1 DFT (and its coset / inverse) is the identity
+    check_canonical(d_data, 1, chk, st);
+    return flag_result() == ZK_OK ? ZK_OK : ZK_ERR_ARG;
+  }
   NttDomain& dom = ctx->domain(log_n);
   ctx->tmp_fr.ensure(sizeof(Fr) * 2 * n);
   Fr* a = ctx->tmp_fr.as<Fr>();
@@ -371,17 +389,17 @@ static int ntt_device(zk_ctx* ctx, void* d_data, uint32_t log_n, int dir, const 
       fr_powers(b, to_dev(host::fr_to_mont(coset->l)), to_dev(one), n, st);
       ltab = b;
     }
-    ntt_natural(d, d, a, dom, false, st, &ctx->prof, ltab, nullptr, nullptr);
+    ntt_natural(d, d, a, dom, false, st, &ctx->prof, ltab, nullptr, nullptr, chk);
   } else if (coset) {                              // out_i *= n^-1 g^-i, fused into the last pass's store
     host::Fr g = host::fr_to_mont(coset->l);
     if (host::fr_is_zero(g)) return ZK_ERR_ARG;
     fr_powers(b, to_dev(host::fr_inv(g)), to_dev(ninv), n, st);
-    ntt_natural(d, d, a, dom, true, st, &ctx->prof, nullptr, b, nullptr);
+    ntt_natural(d, d, a, dom, true, st, &ctx->prof, nullptr, b, nullptr, chk);
   } else {
     const Fr c = to_dev(ninv);
-    ntt_natural(d, d, a, dom, true, st, &ctx->prof, nullptr, nullptr, &c);
+    ntt_natural(d, d, a, dom, true, st, &ctx->prof, nullptr, nullptr, &c, chk);
   }
-  return ZK_OK;
+  return flag_result();
 }
 
 int zk_ntt_fr_dev(zk_ctx* ctx, void* d_data, uint32_t log_n, int dir, const zk_fr* coset) {
@@ -498,8 +516,37 @@ int zk_ctx_attach_rccl(zk_ctx* ctx, const uint8_t unique_id[128], int rank, int 
   if (!ctx || !unique_id || world < 1 || rank < 0 || rank >= world) return ZK_ERR_ARG;
   ZK_GUARD(ctx, {
     ctx->exch = make_rccl_exchange(unique_id, rank, world);
+    ctx->exch->timeout_ms = ctx->exch_timeout_ms;
     return ZK_OK;
   })
+}
+
+int zk_ctx_attach_exchange(zk_ctx* ctx, const zk_exchange_ops* ops, int rank, int world) {
+  if (!ctx || !ops || !ops->all_to_all || !ops->all_reduce_max || world < 1 || rank < 0 || rank >= world)
+    return ZK_ERR_ARG;
+  ZK_GUARD(ctx, {
+    ctx->exch = make_host_exchange(*ops, rank, world);
+    ctx->exch->timeout_ms = ctx->exch_timeout_ms;
+    return ZK_OK;
+  })
+}
+
+int zk_groth16_witness_ranges(zk_ctx* ctx, const zk_pk_dev* pk, uint64_t* ranges, size_t cap, size_t* nranges) {
+  if (!ctx || !pk || !nranges || (cap && !ranges)) return ZK_ERR_ARG;
+  const std::vector<uint64_t> w = witness_ranges(ctx, pk);
+  *nranges = w.size() / 2;
+  for (size_t k = 0; k < std::min(cap, w.size() / 2); k++) {
+    ranges[2 * k] = w[2 * k];
+    ranges[2 * k + 1] = w[2 * k + 1];
+  }
+  return ZK_OK;
+}
+
+int zk_groth16_prove_partial_host(zk_ctx* ctx, const zk_pk_dev* pk, const zk_fr* z_slice, size_t slice_len,
+                                  size_t zlen, size_t num_public, const zk_fr* r, const zk_fr* s,
+                                  zk_prove_partial* out) {
+  if (!ctx || !pk || !r || !s || !out) return ZK_ERR_ARG;
+  ZK_GUARD(ctx, { return prove_partial_host_impl(ctx, pk, z_slice, slice_len, zlen, num_public, r, s, out); })
 }
 
 int zk_test_prove_virtual_shards(zk_ctx* ctx, const zk_pk_dev* const* shards, uint32_t nshards, const void* d_z,

@@ -100,17 +100,16 @@ struct Prof {
     uint64_t units;
     hipStream_t st;
   };
-  // Timeline (tuning): with ZK_TIMELINE=<file>, collect() appends one line
-  // per phase -- name, stream, start and end in ms after the last
-  // mark_origin() -- so an unprofiled run shows how the streams overlap.
+  // Timeline (zk_ctx_profile(ctx, 2), read by zk_ctx_timeline_read):
+  // collect() appends one line per phase -- name, stream, start and end in
+  // ms after the last mark_origin() -- and "--" per collection, so a run
+  // shows how the streams overlap.
+  bool timeline = false;
+  std::string tl;
   hipEvent_t origin = nullptr;
   bool origin_set = false;
-  const char* timeline_path() {
-    static const char* p = getenv("ZK_TIMELINE");
-    return p;
-  }
   void mark_origin(hipStream_t st) {
-    if (!on || !timeline_path()) return;
+    if (!on || !timeline) return;
     if (!origin) ZK_HIP(hipEventCreate(&origin));
     ZK_HIP(hipEventRecord(origin, st));
     origin_set = true;
@@ -150,16 +149,18 @@ struct Prof {
   }
   // after the stream has been synchronised
   void collect() {
-    FILE* tl = (origin_set && timeline_path()) ? fopen(timeline_path(), "a") : nullptr;
+    const bool rec_tl = origin_set && timeline;
     for (Rec& r : pending) {
       float ms = 0;
       ZK_HIP(hipEventSynchronize(r.b));
       ZK_HIP(hipEventElapsedTime(&ms, r.a, r.b));
-      if (tl) {
+      if (rec_tl) {
         float t0 = 0, t1 = 0;
         ZK_HIP(hipEventElapsedTime(&t0, origin, r.a));
         ZK_HIP(hipEventElapsedTime(&t1, origin, r.b));
-        fprintf(tl, "%s %p %.4f %.4f\n", r.phase.c_str(), (void*)r.st, t0, t1);
+        char line[256];
+        snprintf(line, sizeof line, "%s %p %.4f %.4f\n", r.phase.c_str(), (void*)r.st, t0, t1);
+        tl += line;
       }
       PhaseStat& s = stats[r.phase];
       s.ms += ms;
@@ -169,10 +170,7 @@ struct Prof {
       pool.push_back(r.b);
     }
     pending.clear();
-    if (tl) {
-      fprintf(tl, "--\n");
-      fclose(tl);
-    }
+    if (rec_tl) tl += "--\n";
     origin_set = false;
   }
   ~Prof() {

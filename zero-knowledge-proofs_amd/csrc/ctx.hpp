@@ -29,9 +29,8 @@ struct zk_ctx {
   int device = 0;
   hipStream_t stream = nullptr;                 // main stream
   hipStream_t side[zk::NUM_SIDE] = {};          // G2 / IC / A+B1 MSM streams
-  hipEvent_t ev_quot = nullptr, ev_scal = nullptr, ev_hsort = nullptr;
+  hipEvent_t ev_scal = nullptr;                 // witness checked (flags reset)
   hipEvent_t ev_done[zk::NUM_MSM] = {};         // per-MSM completion (results downloaded)
-  hipEvent_t ev_acc[zk::NUM_MSM] = {};          // per-MSM accumulate done (chained schedule 8)
   std::string err;
   zk::MsmWork msm[zk::NUM_MSM];
   std::map<uint32_t, std::unique_ptr<zk::NttDomain>> domains;
@@ -39,11 +38,16 @@ struct zk_ctx {
   zk::DevBuf z_canon, z_mont, qa, qb, qc, flags;
   zk::PinnedBuf flags_host;
   zk::DevBuf scal[zk::NUM_MSM];
-  zk::DevBuf tmp_bases, tmp_scal, tmp_fr;
+  zk::DevBuf tmp_scal, tmp_fr;
   zk::Prof prof;
   std::unique_ptr<zk::Exchange> exch;          // RCCL communicator (sharded prover), if attached
   zk::DistQ dq;                                // distributed-quotient buffers
-  int sched = -1;                              // zk_ctx_set_schedule (-1: ZK_PROVE_SCHED / default)
+  // Explicit choices (zk_ctx_set_schedule / zk_ctx_set_option); never read
+  // from the environment, and no proof depends on them.
+  int sched = 0;                               // 0 overlapped streams, 3 serial (per-kernel timing)
+  int quot_path = -1;                          // -1 by domain size, 0 small-domain, 1 large-domain
+  int prove_win_c = 0;                         // 0 by size, else 16 or 22 (keys made after the call)
+  double exch_timeout_ms = 60000;              // watchdog of an attached exchange
 
   zk::NttDomain& domain(uint32_t log_n);
 };
@@ -66,16 +70,29 @@ struct zk_pk_dev {
   // Bytes between consecutive bases of bases[slot]: 0 = packed (sizeof the
   // affine point), else padded to whole 128-B lines (msm_pad_bases).
   uint32_t stride[zk::NUM_MSM] = {};
+  // [lo, hi) pairs: the z entries this shard reads with a distributed
+  // quotient (zk_groth16_witness_ranges); without one it reads all of z
+  std::vector<uint64_t> wr_dist;
 };
 
 namespace zk {
 // Expand every slot's bases into the window-shifted copies the shared-bucket
-// MSM reads (ZK_MSM_PRECOMP=0 keeps one copy and per-window buckets).
+// MSM reads.
 void pk_precompute_windows(zk_ctx* ctx, zk_pk_dev& pk);
 // canonical-input checks (prove.hip): a < r on the host; on the device,
 // flags |= 8 when some of the n canonical Fr at d_z is >= r
 bool fr_canonical(const zk_fr& a);
 void check_canonical(const void* d_z, uint64_t n, uint32_t* d_flags, hipStream_t st);
+// the witness ranges of a finished key (its idx vectors and shard) from the
+// host constraint matrices: fills pk.wr_dist
+void pk_witness_ranges(zk_pk_dev& pk, const zk_r1cs_csr* q, hipStream_t st);
+// Which shard holds variable v's A / B1 / B2 / IC bases: with a distributed
+// quotient possible (nshards 2, 4 or 8, n % nshards^2 == 0) the shard whose
+// quotient rows first reference v, so a rank's MSM variables are the ones
+// its quotient rows read anyway and its witness slice is ~1/nshards of z;
+// unreferenced variables by contiguous range.  Empty: contiguous ranges of
+// every base vector.
+std::vector<uint8_t> var_owner(const zk_r1cs_csr* q, uint64_t n, uint32_t nshards);
 }
 
 struct zk_msm_bases {

@@ -13,7 +13,9 @@
 //      omega_n^(-c e)                           -> exchange 3 (q per rank)
 //   D  row c = r: size-m inverse DFT, n^-1 g^-i, lo64 -> H_(r + N d)
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <thread>
 
 #include "dist.hpp"
 #include "quotient.hpp"
@@ -226,7 +228,7 @@ void dq_stage_b(zk_ctx* ctx, const zk_pk_dev* pk, int rank, int world, DistQ& dq
   k_dq_rows<<<ceil_div(3 * m, 256), 256, 0, st>>>(dq.r1.as<Fr>(), m, q, rows);
   ZK_LAUNCH_CHECK();
   for (int v = 0; v < 3; v++) ntt_dif(rows + v * m, dm, /*inverse*/ true, st, &ctx->prof);   // n A_i, bit-reversed
-  k_dq_coset<<<ceil_div(3 * m, 256), 256, 0, st>>>(rows, dn.gpow.as<Fr>(), rank, world, m, log_m);
+  k_dq_coset<<<ceil_div(3 * m, 256), 256, 0, st>>>(rows, domain_gpow(dn, st), rank, world, m, log_m);
   ZK_LAUNCH_CHECK();
   for (int v = 0; v < 3; v++) ntt_dit(rows + v * m, dm, /*inverse*/ false, st, &ctx->prof);  // natural e
   k_dq_send2<<<ceil_div(3 * m, 256), 256, 0, st>>>(rows, rank, m, q, tabs_of(dn, false), pk->log_n,
@@ -258,20 +260,48 @@ void dq_stage_d(zk_ctx* ctx, const zk_pk_dev* pk, int rank, int world, DistQ& dq
   NttDomain& dn = ctx->domain(pk->log_n);
   NttDomain& dm = ctx->domain(log_m);
   ntt_dif(dq.r3.as<Fr>(), dm, /*inverse*/ true, st, &ctx->prof);
-  k_dq_h<<<ceil_div(m, 256), 256, 0, st>>>(dq.r3.as<Fr>(), dn.gipow.as<Fr>(), rank, world, m, log_m, h_out);
+  k_dq_h<<<ceil_div(m, 256), 256, 0, st>>>(dq.r3.as<Fr>(), domain_gipow(dn, st), rank, world, m, log_m, h_out);
   ZK_LAUNCH_CHECK();
+}
+
+void dq_prepare(zk_ctx* ctx, const zk_pk_dev* pk, int world, DistQ& dq, hipStream_t st) {
+  ensure_bufs(pk, world, dq);
+  NttDomain& dn = ctx->domain(pk->log_n);
+  (void)ctx->domain((uint32_t)log2i(pk->n / world));
+  domain_gpow(dn, st);
+  domain_gipow(dn, st);
+  ZK_HIP(hipStreamSynchronize(st));
 }
 
 void dist_quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, Exchange& ex, DistQ& dq,
                    uint32_t* d_flags, uint64_t* h_out, hipStream_t st) {
   const int r = ex.rank, N = ex.world;
+  const int fault = ex.fault_after;
+  ex.fault_after = 0;   // one proof
+  auto exchange = [&](int k, const DevBuf& s, DevBuf& rv) {
+    ex.all_to_all(s.p, rv.p, dq_chunk_bytes(pk, N, k), st);
+    if (fault == k) throw Error(ZK_ERR_DEVICE, "injected fault after exchange " + std::to_string(k));
+  };
   dq_stage_a(ctx, pk, d_z, r, N, dq, d_flags, st);
-  ex.all_to_all(dq.s1.p, dq.r1.p, dq_chunk_bytes(pk, N, 1), st);
+  exchange(1, dq.s1, dq.r1);
   dq_stage_b(ctx, pk, r, N, dq, st);
-  ex.all_to_all(dq.s2.p, dq.r2.p, dq_chunk_bytes(pk, N, 2), st);
+  exchange(2, dq.s2, dq.r2);
   dq_stage_c(ctx, pk, r, N, dq, st);
-  ex.all_to_all(dq.s3.p, dq.r3.p, dq_chunk_bytes(pk, N, 3), st);
+  exchange(3, dq.s3, dq.r3);
   dq_stage_d(ctx, pk, r, N, dq, h_out, st);
+}
+
+void sync_watchdog(hipStream_t st, Exchange& ex) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipStreamQuery(st);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) ZK_HIP(q);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (ex.async_error()) throw Error(ZK_ERR_RCCL, "exchange: asynchronous transport error");
+    if (ms > ex.timeout_ms) throw Error(ZK_ERR_RCCL, "exchange: a peer did not answer within the timeout");
+    std::this_thread::yield();
+  }
 }
 
 // --------------------------------------------------------------- RCCL ---
@@ -296,13 +326,65 @@ struct RcclExchange : Exchange {
     ZK_HIP(hipMemcpyAsync(stat.p, stat_host.p, 4, hipMemcpyHostToDevice, st));
     ZK_NCCL(ncclAllReduce(stat.p, stat.p, 1, ncclInt32, ncclMax, comm, st));
     ZK_HIP(hipMemcpyAsync(stat_host.p, stat.p, 4, hipMemcpyDeviceToHost, st));
-    ZK_HIP(hipStreamSynchronize(st));
+    sync_watchdog(st, *this);
     return *stat_host.as<int32_t>();
+  }
+  // ncclCommAbort sets the communicator's abort flag, which its in-flight
+  // kernels poll: this rank's collectives end, and so do the peers' once
+  // their own watchdog (prove.hip) aborts them.
+  void abort() override {
+    if (comm) (void)ncclCommAbort(comm);
+    comm = nullptr;
+  }
+  bool async_error() override {
+    if (!comm) return true;
+    ncclResult_t r = ncclSuccess;
+    return ncclCommGetAsyncError(comm, &r) != ncclSuccess || (r != ncclSuccess && r != ncclInProgress);
   }
   ~RcclExchange() override {
     if (comm) (void)ncclCommDestroy(comm);
   }
 };
+
+// ---------------------------------------------------------- host-staged ---
+// Each all-to-all: the send chunks come back to pinned host memory (after the
+// stream's preceding kernels), the caller's callback moves them between the
+// ranks, and the received chunks go back to the device ahead of the next
+// stage.  Synchronous on the calling thread; the other streams (the MSMs)
+// keep running meanwhile.  A callback error or a non-zero status becomes
+// ZK_ERR_RCCL.
+struct HostExchange : Exchange {
+  zk_exchange_ops ops{};
+  PinnedBuf send_h, recv_h;
+  void all_to_all(const void* send, void* recv, size_t chunk_bytes, hipStream_t st) override {
+    const size_t bytes = chunk_bytes * (size_t)world;
+    send_h.ensure(bytes);
+    recv_h.ensure(bytes);
+    ZK_HIP(hipMemcpyAsync(send_h.p, send, bytes, hipMemcpyDeviceToHost, st));
+    ZK_HIP(hipStreamSynchronize(st));
+    if (ops.all_to_all(ops.user, send_h.p, recv_h.p, chunk_bytes) != 0)
+      throw Error(ZK_ERR_RCCL, "host exchange: all_to_all callback failed");
+    ZK_HIP(hipMemcpyAsync(recv, recv_h.p, bytes, hipMemcpyHostToDevice, st));
+  }
+  int agree_max(int status, hipStream_t st) override {
+    (void)st;
+    int32_t v = status;
+    if (ops.all_reduce_max(ops.user, &v) != 0) throw Error(ZK_ERR_RCCL, "host exchange: all_reduce_max callback failed");
+    return v;
+  }
+  void abort() override {
+    if (ops.abort) ops.abort(ops.user);
+  }
+};
+
+std::unique_ptr<Exchange> make_host_exchange(const zk_exchange_ops& ops, int rank, int world) {
+  if (!ops.all_to_all || !ops.all_reduce_max) throw Error(ZK_ERR_ARG, "host exchange: missing callbacks");
+  std::unique_ptr<HostExchange> ex(new HostExchange());
+  ex->ops = ops;
+  ex->rank = rank;
+  ex->world = world;
+  return ex;
+}
 
 static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
 

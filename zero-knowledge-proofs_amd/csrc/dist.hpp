@@ -24,12 +24,29 @@ struct zk_pk_dev;
 namespace zk {
 
 // All-to-all of equal chunks: chunk k of `send` goes to rank k, chunk s of
-// `recv` comes from rank s.
+// `recv` comes from rank s.  Two transports: RCCL (ncclAllToAll over xGMI,
+// enqueued on the stream) and host-staged callbacks (zk_exchange_ops: the
+// chunks cross through pinned host memory and the caller's transport, e.g.
+// torch.distributed over gloo).
 struct Exchange {
   int rank = 0, world = 1;
+  // set once a proof failed after the ranks agreed to start: the peers may
+  // be blocked in (or have abandoned) a collective, so the exchange is dead
+  bool broken = false;
   virtual void all_to_all(const void* send, void* recv, size_t chunk_bytes, hipStream_t st) = 0;
   // max over ranks of a host status code (synchronous)
   virtual int agree_max(int status, hipStream_t st) = 0;
+  // make the peers' pending collectives with this rank fail instead of
+  // waiting forever (RCCL: ncclCommAbort; host: the caller's abort callback)
+  virtual void abort() = 0;
+  // an asynchronous transport error is pending (RCCL: ncclCommGetAsyncError)
+  virtual bool async_error() { return false; }
+  // watchdog for waits on work that depends on the peers: give up (throw
+  // ZK_ERR_RCCL) after this long or on an asynchronous transport error
+  double timeout_ms = 60000;
+  // test hook (zk_ctx_set_option ZK_OPT_FAULT_AFTER_EXCHANGE): throw after
+  // the k-th all-to-all of the next proof, as a rank-local failure would
+  int fault_after = 0;
   virtual ~Exchange() = default;
 };
 
@@ -53,12 +70,20 @@ void dq_stage_d(zk_ctx* ctx, const zk_pk_dev* pk, int rank, int world, DistQ& q,
 // chunk bytes of the three exchanges
 size_t dq_chunk_bytes(const zk_pk_dev* pk, int world, int which);
 
-// The whole pipeline with a live exchange (RCCL): stage, all-to-all, ...
+// The whole pipeline with a live exchange: stage, all-to-all, ...
 void dist_quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, Exchange& ex, DistQ& q,
                    uint32_t* d_flags, uint64_t* h_out, hipStream_t st);
+// Every allocation and table the pipeline will need, made BEFORE the ranks
+// agree to start (an allocation failure then becomes the agreed status, not
+// a rank leaving its peers inside a collective).
+void dq_prepare(zk_ctx* ctx, const zk_pk_dev* pk, int world, DistQ& q, hipStream_t st);
 
 // RCCL communicator wrapper (ncclAllToAll, bytes as ncclUint8).
 std::unique_ptr<Exchange> make_rccl_exchange(const uint8_t unique_id[128], int rank, int world);
 void rccl_unique_id(uint8_t out[128]);
+// Wait for stream st, polling: throws ZK_ERR_RCCL once ex's watchdog fires.
+void sync_watchdog(hipStream_t st, Exchange& ex);
+// Host-staged exchange over the caller's callbacks.
+std::unique_ptr<Exchange> make_host_exchange(const zk_exchange_ops& ops, int rank, int world);
 
 }  // namespace zk

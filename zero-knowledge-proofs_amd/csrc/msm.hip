@@ -6,7 +6,6 @@
 #include <type_traits>
 #include <vector>
 
-#include "lazy.hpp"
 #include "msm.hpp"
 
 namespace zk {
@@ -32,8 +31,6 @@ MsmPlan msm_make_plan(uint32_t n, int bits, int sw, int force_c) {
     if (cost < best) { best = cost; best_c = c; }
   }
   if (force_c) best_c = force_c;
-  // tuning override (tools/phase_bench.py sweeps)
-  if (const char* e = getenv("ZK_MSM_C")) best_c = std::max(4, std::min(16, atoi(e)));
   p.c = best_c;
   p.nwin = (bits + p.c - 1) / p.c;
 
@@ -129,63 +126,6 @@ __device__ __forceinline__ uint32_t scal_window(const uint64_t (&s)[SW], int off
   return (uint32_t)(lo & ((1ull << width) - 1));
 }
 
-// Signed recoding: windows 0..nwin-2 give digits in [-(2^(c-1)-1), 2^(c-1)]
-// with a carry into the next window; the top window absorbs the final carry
-// unsigned (digit in [0, 2^top]), so no extra carry window is needed.
-template <int SW, bool SCATTER>
-__global__ void __launch_bounds__(256) k_msm_digits(const uint64_t* __restrict__ sc, MsmPlan p,
-                                                    uint32_t* __restrict__ counts,
-                                                    uint32_t* __restrict__ cursor,
-                                                    uint32_t* __restrict__ ent,
-                                                    uint32_t* __restrict__ key) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int lane = (int)(threadIdx.x & 63);
-  if (i >= p.n) return;   // whole trailing lanes only: the ballots below see the live ones
-  uint64_t s[SW];
-#pragma unroll
-  for (int k = 0; k < SW; k++) s[k] = sc[(size_t)i * SW + k];
-  uint32_t carry = 0;
-  const uint32_t half = 1u << (p.c - 1);
-  for (int w = 0; w < p.nwin; w++) {
-    const bool top = (w == p.nwin - 1);
-    const int width = top ? p.bits - p.c * w : p.c;
-    uint32_t v = scal_window<SW>(s, p.c * w, width) + carry;
-    uint32_t mag;
-    bool neg = false;
-    if (!top && v > half) {
-      mag = (1u << p.c) - v;  // digit = v - 2^c < 0
-      neg = true;
-      carry = 1;
-    } else {
-      mag = v;
-      carry = 0;
-    }
-    // Wave-aggregated atomics: the lanes sharing the first active lane's
-    // bucket take one atomic between them.  Skewed scalars (a witness of
-    // mostly ones) otherwise serialise ~n atomics on a single counter.
-    const uint32_t gg = mag ? p.boff[w] + mag - 1 : 0xffffffffu;
-    const uint32_t lead = __builtin_amdgcn_readfirstlane(gg);
-    const uint64_t same = __ballot(gg == lead);
-    const int lead_lane = __builtin_ctzll(same);
-    const bool agg = lead != 0xffffffffu && gg == lead;
-    uint32_t base = 0;
-    if (agg && lane == lead_lane)
-      base = atomicAdd(SCATTER ? &cursor[lead] : &counts[lead], (uint32_t)__builtin_popcountll(same));
-    if (SCATTER) {
-      base = __shfl(base, lead_lane);
-      uint32_t pos;
-      if (agg) pos = base + (uint32_t)__builtin_popcountll(same & ((1ull << lane) - 1));
-      else if (gg != 0xffffffffu) pos = atomicAdd(&cursor[gg], 1u);
-      if (gg != 0xffffffffu) {
-        ent[pos] = i | (neg ? 0x80000000u : 0u);
-        key[pos] = gg;
-      }
-    } else if (!agg && gg != 0xffffffffu) {
-      atomicAdd(&counts[gg], 1u);
-    }
-  }
-}
-
 constexpr uint32_t MSM_DUMMY = 0x7fffffffu;   // entry that contributes nothing
 
 // Radix-sort path: one (bucket, entry) pair per (point, window), written
@@ -240,75 +180,6 @@ __global__ void __launch_bounds__(256) k_msm_offsets(const uint32_t* __restrict_
   const uint32_t lo = i ? min(key[i - 1], G) + 1 : 0;     // keys in (key[i-1], key[i]] start at i
   const uint32_t hi = i < M ? min(key[i], G) : G;
   for (uint32_t g = lo; g <= hi; g++) off[g] = i;
-}
-
-// --------------------------------------------------------------- scan ---
-// 3-phase exclusive scan of G bucket counts: per-block sums, one scan of
-// the block sums, per-block scan with its base.  Writes off[0..G] and a
-// copy in cursor[] for the scatter.
-__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sh, uint32_t& total) {
-  const uint32_t t = threadIdx.x;
-  sh[t] = v;
-  __syncthreads();
-  for (uint32_t d = 1; d < 256; d <<= 1) {
-    uint32_t x = t >= d ? sh[t - d] : 0;
-    __syncthreads();
-    sh[t] += x;
-    __syncthreads();
-  }
-  total = sh[255];
-  uint32_t r = sh[t] - v;
-  __syncthreads();
-  return r;
-}
-__global__ void __launch_bounds__(256) k_scan_local(const uint32_t* __restrict__ counts, uint32_t G,
-                                                    uint32_t* __restrict__ part) {
-  __shared__ uint32_t sh[256];
-  const uint32_t base = blockIdx.x * MSM_SCAN_BLOCK + threadIdx.x * 4;
-  uint32_t s = 0;
-#pragma unroll
-  for (int k = 0; k < 4; k++) s += base + k < G ? counts[base + k] : 0;
-  uint32_t tot;
-  block_excl_scan256(s, sh, tot);
-  if (threadIdx.x == 0) part[blockIdx.x] = tot;
-}
-__global__ void __launch_bounds__(1024) k_scan_part(uint32_t* __restrict__ part, uint32_t nblk) {
-  __shared__ uint32_t sh[1024];
-  const uint32_t t = threadIdx.x;
-  const uint32_t v = t < nblk ? part[t] : 0;
-  sh[t] = v;
-  __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {
-    uint32_t x = t >= d ? sh[t - d] : 0;
-    __syncthreads();
-    sh[t] += x;
-    __syncthreads();
-  }
-  if (t < nblk) part[t] = sh[t] - v;
-}
-__global__ void __launch_bounds__(256) k_scan_down(uint32_t* __restrict__ counts, uint32_t G,
-                                                   const uint32_t* __restrict__ part, uint32_t* __restrict__ off,
-                                                   uint32_t* __restrict__ cur) {
-  __shared__ uint32_t sh[256];
-  const uint32_t base = blockIdx.x * MSM_SCAN_BLOCK + threadIdx.x * 4;
-  uint32_t c[4], s = 0;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    c[k] = base + k < G ? counts[base + k] : 0;
-    if (base + k < G) counts[base + k] = 0;   // ready for the next MSM on this workspace
-    s += c[k];
-  }
-  uint32_t tot;
-  uint32_t x = block_excl_scan256(s, sh, tot) + part[blockIdx.x];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    if (base + k < G) {
-      off[base + k] = x;
-      cur[base + k] = x;
-    }
-    if (base + k == G - 1) off[G] = x + c[k];
-    x += c[k];
-  }
 }
 
 // --------------------------------------------------------- accumulate ---
@@ -384,7 +255,7 @@ ZK_DI const A* seg_base(const SegBases<A>& sb, uint32_t seg, uint32_t i) {
 }
 
 template <class C>
-__global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum(SegBases<typename C::A> sb, uint32_t segshift, uint32_t idx_mask,
+__global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum(SegBases<typename C::A> sb, uint32_t segshift,
                                                    const uint32_t* __restrict__ ent,
                                                    const uint32_t* __restrict__ key,
                                                    const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
@@ -415,7 +286,7 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum(SegBases<typena
     }
     if (en == MSM_DUMMY) continue;   // zero digit (shared-bucket plans)
     // batch: bucket g >> segshift names the MSM whose bases entry en indexes
-    typename C::A a = ld_vec(seg_base(sb, g >> segshift, en & idx_mask));
+    typename C::A a = ld_vec(seg_base(sb, g >> segshift, en));
     if (en & 0x80000000u) a.y = f_neg(a.y);
     if (!aff_is_inf(a)) acc = xyzz_madd(acc, a);
   }
@@ -424,73 +295,6 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum(SegBases<typena
   if (head) st_vec(&partials[2 * (size_t)t], acc);
   else if (tail) st_vec(&partials[2 * (size_t)t + 1], acc);
   else st_vec(&buckets[cur], acc);
-}
-
-// G1 accumulate in lazy.hpp's redundant Fq form: the same chunks, loop,
-// branches and flushes as k_msm_accum<G1>; the accumulator stays in signed
-// 28-bit limbs between adds and is made canonical only when flushed.
-ZK_DI void st_lazy(G1X* p, const FlX& a) {
-  st_vec(&p->X, fl_to_fq(a.X));
-  ZK_SB();
-  st_vec(&p->Y, fl_to_fq(a.Y));
-  ZK_SB();
-  st_vec(&p->ZZ, fl_to_fq(a.ZZ));
-  ZK_SB();
-  st_vec(&p->ZZZ, fl_to_fq(a.ZZZ));
-}
-#ifndef ZK_LAZY_WPE
-#define ZK_LAZY_WPE 3
-#endif
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(ZK_LAZY_WPE))) k_msm_accum_g1l(SegBases<G1A> sb, uint32_t segshift,
-                                                                    uint32_t idx_mask,
-                                                                    const uint32_t* __restrict__ ent,
-                                                                    const uint32_t* __restrict__ key,
-                                                                    const uint32_t* __restrict__ off, uint32_t G,
-                                                                    uint32_t T, G1X* __restrict__ buckets,
-                                                                    G1X* __restrict__ partials) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t M = off[G];
-  const uint32_t K = chunk_len(M, T);
-  const uint32_t start = t * K;
-  if (t >= T || start >= M) return;
-  const uint32_t end = min(start + K, M);
-  FlX acc;
-  flx_set_inf(acc);
-  uint32_t cur = key[start], run_start = start;
-  __shared__ uint32_t entq_lds[2 * ENTQ_LDS_WORDS];   // 128 threads = 2 waves
-  EntQ q(entq_lds);
-  for (uint32_t e = start; e < end; e++) {
-    uint32_t g, en;
-    q.next(key, ent, start, e, g, en);
-    if (g != cur) {
-      const bool head = (run_start == start) && (off[cur] < start);
-      st_lazy(head ? &partials[2 * (size_t)t] : &buckets[cur], acc);
-      flx_set_inf(acc);
-      cur = g;
-      run_start = e;
-    }
-    if (en == MSM_DUMMY) continue;
-    const G1A a = ld_vec(seg_base(sb, g >> segshift, en & idx_mask));
-    if (aff_is_inf(a)) continue;
-    FlA la{fl_from_fq(a.x), fl_from_fq(a.y)};
-    if (en & 0x80000000u) la.y = fl_neg(la.y);
-    acc = flx_madd(acc, la);
-  }
-  const bool head = (run_start == start) && (off[cur] < start);
-  const bool tail = off[cur + 1] > end;
-  st_lazy(head ? &partials[2 * (size_t)t] : tail ? &partials[2 * (size_t)t + 1] : &buckets[cur], acc);
-}
-// ZK_LAZY_ACCUM=1 selects k_msm_accum_g1l (experiment, off by default):
-// ~10% fewer VALU instructions per madd than k_msm_accum<G1>, but the
-// signed product columns need more registers (227 VGPRs unconstrained, 168
-// with 25 spilled at 3 waves/SIMD) and the prove is no faster (9.93 vs
-// 9.97 ms, 2 waves: 10.15 ms).
-static bool g1_lazy_mode() {
-  static const bool v = [] {
-    const char* e = getenv("ZK_LAZY_ACCUM");
-    return e && std::strcmp(e, "1") == 0;
-  }();
-  return v;
 }
 
 // G2 accumulate over lane pairs (Fq2h, ff.hpp): chunk t is owned by lanes
@@ -505,7 +309,6 @@ ZK_DI void st_pair(G2X* p, const XYZZ<Fq2h>& a) {
   st_vec(q + 6, a.ZZZ.v);
 }
 __global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum_pair(SegBases<G2A> sb, uint32_t segshift,
-                                                                      uint32_t idx_mask,
                                                                       const uint32_t* __restrict__ ent,
                                                                       const uint32_t* __restrict__ key,
                                                                       const uint32_t* __restrict__ off, uint32_t G,
@@ -535,7 +338,7 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum_pair(SegBases<G
       run_start = e;
     }
     if (en == MSM_DUMMY) continue;
-    const Fq* bp = reinterpret_cast<const Fq*>(seg_base(sb, g >> segshift, en & idx_mask)) + h;
+    const Fq* bp = reinterpret_cast<const Fq*>(seg_base(sb, g >> segshift, en)) + h;
     Affine<Fq2h> a{{ld_vec(bp)}, {ld_vec(bp + 2)}};
     if (en & 0x80000000u) a.y = f_neg(a.y);
     if (!aff_is_inf(a)) acc = xyzz_madd(acc, a);
@@ -547,24 +350,10 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum_pair(SegBases<G
   else st_pair(&buckets[cur], acc);
 }
 
-// G1 row/column sums over lane quads when there are at most this many sums
-// (ZK_RC_QUAD_MAX): few sums leave most SIMDs idle, so the 4x lanes are free
-static uint32_t rowcol_quad_max() {
-  static const uint32_t v = [] {
-    const char* e = getenv("ZK_RC_QUAD_MAX");
-    return e ? (uint32_t)strtoul(e, nullptr, 0) : 600u;   // single-window G1 MSMs (H: 512 sums)
-  }();
-  return v;
-}
-
-// ZK_G2_PAIR=0 keeps the one-lane G2 accumulate (A/B switch)
-static bool g2_pair_mode() {
-  static const bool on = [] {
-    const char* e = getenv("ZK_G2_PAIR");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
+// G1 row/column sums over lane quads when there are at most this many sums:
+// few sums leave most SIMDs idle, so the 4x lanes are free (single-window
+// G1 MSMs, e.g. H: 512 sums)
+constexpr uint32_t ROWCOL_QUAD_MAX = 600;
 
 // Buckets whose entries span several accumulate chunks.  A bucket over
 // P = t1 - t0 + 1 chunks is tail(t0) + head(t0+1) + ... + head(t1):
@@ -788,22 +577,12 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_quant(MsmPlan p, con
 // j + 16 RW, ... serially, a 4-step __shfl_xor butterfly (lane distances
 // 4..32 keep each lane's quad position) combines a wave, then waves 1..RW-1
 // hand their totals to wave 0 through LDS.  One xyzz_add_quad call site.
-// ZK_RED_QUAD (build-time mask): 1 = quantities, 2 = row/column sums,
-// 4 = G1 fixup use the quad kernels; ZK_RED_QWAVES waves per quad sum.
-#ifndef ZK_RED_QUAD
-#define ZK_RED_QUAD 1
-#endif
+// The quantities (tens of sums) always run on quads; the G1 row/column sums
+// when there are few of them (ROWCOL_QUAD_MAX).  ZK_RED_QWAVES (build flag)
+// waves per quad sum.
 #ifndef ZK_RED_QWAVES
 #define ZK_RED_QWAVES 4
 #endif
-// the env variable of the same name overrides the build-time mask (A/B runs)
-static uint32_t red_quad_mask() {
-  static const uint32_t m = [] {
-    const char* e = getenv("ZK_RED_QUAD");
-    return e ? (uint32_t)strtoul(e, nullptr, 0) : (uint32_t)ZK_RED_QUAD;
-  }();
-  return m;
-}
 
 template <class X, int RW>
 __device__ __forceinline__ X quad_sum_step(X v, uint32_t it, uint32_t niter, X* xs, bool have, const X& term) {
@@ -904,32 +683,6 @@ __global__ void __launch_bounds__(64 * RW) k_msm_quant_q(MsmPlan p, const typena
   if (threadIdx.x == 0) st_vec(&res[b], v);
 }
 
-// k_msm_fixup with one quad per bucket (G1: its waves fit 3 per SIMD, so the
-// 4x lanes cost no extra rounds; G2 keeps the one-thread version).
-template <class C>
-__global__ void __launch_bounds__(128) k_msm_fixup_q(const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
-                                                     uint32_t fix_max, uint32_t* __restrict__ nbig,
-                                                     typename C::X* __restrict__ buckets,
-                                                     const typename C::X* __restrict__ partials) {
-  using X = typename C::X;
-  const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;
-  const bool lead = (threadIdx.x & 3) == 0;
-  if (g >= G) return;   // quad-uniform from here on
-  const uint32_t K = chunk_len(off[G], T);
-  const uint32_t bs = off[g], be = off[g + 1];
-  if (be == bs) return;
-  const uint32_t t0 = bs / K, t1 = (be - 1) / K;
-  if (t0 == t1) return;
-  if (t1 - t0 + 1 > fix_max) {
-    if (lead) atomicAdd(nbig, 1u);
-    return;
-  }
-  X acc = ld_vec(&partials[2 * (size_t)t0 + 1]);
-#pragma unroll 1
-  for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add_quad(acc, ld_vec(&partials[2 * (size_t)t]));
-  if (lead) st_vec(&buckets[g], acc);
-}
-
 // ---- lane-pair G2 reductions (Fq2h) -------------------------------------
 // G2 row/column sums and fixup with each add split over a lane pair: half the
 // registers (two waves per SIMD) and half the multiply chain per add on the
@@ -998,61 +751,47 @@ __global__ void __launch_bounds__(128) k_msm_fixup_pair(const uint32_t* __restri
 void sort_pairs_u32(void* tmp, size_t& tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
                     const uint32_t* vals_in, uint32_t* vals_out, size_t n, unsigned end_bit, hipStream_t st);
 
-// 0: rocPRIM radix sort (default), 1: atomic counting sort (ZK_MSM_SORT=count)
-static int msm_sort_mode() {
-  static const int mode = [] {
-    const char* e = getenv("ZK_MSM_SORT");
-    return (e && std::strcmp(e, "count") == 0) ? 1 : 0;
-  }();
-  return mode;
-}
-
 // Accumulate threads: one full-occupancy round of the chip (blocks per CU
-// from the occupancy calculator x CUs x 128), x ZK_MSM_ROUNDS for tuning.
+// from the occupancy calculator x CUs x 128; G2 runs two lanes per chunk).
 template <class C>
 static uint32_t accum_threads() {
   static const uint32_t T = [] {
     int dev = 0, cus = 0, per_cu = 0;
     ZK_HIP(hipGetDevice(&dev));
     ZK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const bool pair = std::is_same<C, G2>::value && g2_pair_mode();   // two lanes per chunk
-    if (pair)
+    constexpr bool pair = std::is_same<C, G2>::value;
+    if constexpr (pair)
       ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_accum_pair, 128, 0));
-    else if (std::is_same<C, G1>::value && g1_lazy_mode())
-      ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_accum_g1l, 128, 0));
     else
       ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_accum<C>, 128, 0));
-    double rounds = 1.0;   // tuning: fractions leave room for concurrent streams
-    if (const char* e = getenv("ZK_MSM_ROUNDS")) rounds = std::max(0.05, atof(e));
-    if (const char* e = getenv(std::is_same<C, G2>::value ? "ZK_MSM_ROUNDS_G2" : "ZK_MSM_ROUNDS_G1"))
-      rounds = std::max(0.05, atof(e));
-    return (uint32_t)std::max(1.0, per_cu * cus * (pair ? 64 : 128) * rounds);
+    return (uint32_t)std::max(1, per_cu * cus * (pair ? 64 : 128));
   }();
   return T;
 }
+
+// Buckets spread over at most this many accumulate chunks are summed by the
+// serial fixup; larger ones go through the log-depth merge.
+constexpr uint32_t MSM_FIX_MAX = 8;
 
 // One MSM (nseg = 1) or a batch of MSMs sharing every phase: segment k's
 // keys start at bucket k << segshift and its entries at sum_{j<k} nwin n_j.
 template <class C>
 static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hipStream_t st) {
   using X = typename C::X;
+  constexpr bool g2 = std::is_same<C, G2>::value;
   MsmPlan& p = w.plan;
-  if (p.G > (uint32_t)MSM_SCAN_BLOCK * 1024 && !(msm_sort_mode() == 0 || p.shared))
-    throw Error(ZK_ERR_ARG, "msm: too many buckets for the counting sort");
   if (nseg < 1 || nseg > MSM_MAXSEG || (nseg > 1 && (!p.shared || sw != 1)))
     throw Error(ZK_ERR_ARG, "msm: bad batch");
   size_t M = 0;
   for (int k = 0; k < nseg; k++) M += (size_t)segs[k].n * p.nwin;
   if (M >= 0x80000000ull) throw Error(ZK_ERR_ARG, "msm: too many (point, window) entries");
   const uint32_t n = p.n;   // all points of the batch (profiling units)
-  const uint32_t nblk = ceil_div(p.G, MSM_SCAN_BLOCK);
   w.off.ensure(sizeof(uint32_t) * (p.G + 1));
   w.ent.ensure(sizeof(uint32_t) * (M + ENTQ));   // EntQ reads up to ENTQ - 1 past the end
   w.key.ensure(sizeof(uint32_t) * (M + ENTQ));
   w.buckets.ensure(sizeof(X) * p.G);
   p.T = accum_threads<C>();
-  p.fix_max = 8;
-  if (const char* e = getenv("ZK_MSM_FIX")) p.fix_max = (uint32_t)std::max(1, atoi(e));
+  p.fix_max = MSM_FIX_MAX;
   w.partials.ensure(sizeof(X) * 2 * (size_t)p.T);
   w.partials2.ensure(sizeof(X) * ((size_t)p.T / 2 + 2));
   w.rc.ensure(sizeof(X) * p.nrc);
@@ -1066,120 +805,58 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
   }
 
   Prof* pf = w.prof;
-  const bool g2 = sizeof(typename C::A) == sizeof(G2A);
-  int ph = pf ? pf->begin(st, (w.tag + "msm_sort").c_str(), n) : -1;   // group (point, window) entries by bucket
-  if (msm_sort_mode() == 0 || p.shared) {
-    // rocPRIM radix sort on ceil(log2(G + 1)) key bits (log2(G) when shared)
-    unsigned end_bit = 1;
-    while ((1ull << end_bit) < (uint64_t)p.G + (p.shared ? 0 : 1)) end_bit++;
-    w.key_in.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
-    w.ent_in.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
-    size_t tmp_bytes = 0;
-    sort_pairs_u32(nullptr, tmp_bytes, nullptr, nullptr, nullptr, nullptr, M, end_bit, st);
-    w.sort_tmp.ensure(tmp_bytes);
-    size_t eoff = 0;
-    for (int k = 0; k < nseg; k++) {
-      const uint32_t nk = segs[k].n;
-      if (!nk) continue;
-      const uint32_t nb = ceil_div(nk, 256);
-      const uint32_t kbase = p.shared ? (uint32_t)k << (p.segshift & 31) : 0u;
-      uint32_t* ki = w.key_in.as<uint32_t>() + eoff;
-      uint32_t* ei = w.ent_in.as<uint32_t>() + eoff;
-      if (sw == 1) k_msm_keys<1><<<nb, 256, 0, st>>>(segs[k].scalars, p, nk, nseg > 1 ? kbase : 0u, ki, ei);
-      else k_msm_keys<4><<<nb, 256, 0, st>>>(segs[k].scalars, p, nk, 0u, ki, ei);
-      ZK_LAUNCH_CHECK();
-      eoff += (size_t)nk * p.nwin;
-    }
-    if (M)
-      sort_pairs_u32(w.sort_tmp.p, tmp_bytes, w.key_in.as<uint32_t>(), w.key.as<uint32_t>(),
-                     w.ent_in.as<uint32_t>(), w.ent.as<uint32_t>(), M, end_bit, st);
-    k_msm_offsets<<<ceil_div(M + 1, 256), 256, 0, st>>>(w.key.as<uint32_t>(), (uint32_t)M, p.G, w.off.as<uint32_t>());
+  // group the (point, window) entries by bucket: rocPRIM radix sort on
+  // ceil(log2(G + 1)) key bits (log2(G) when shared)
+  int ph = pf ? pf->begin(st, (w.tag + "msm_sort").c_str(), n) : -1;
+  unsigned end_bit = 1;
+  while ((1ull << end_bit) < (uint64_t)p.G + (p.shared ? 0 : 1)) end_bit++;
+  w.key_in.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
+  w.ent_in.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
+  size_t tmp_bytes = 0;
+  sort_pairs_u32(nullptr, tmp_bytes, nullptr, nullptr, nullptr, nullptr, M, end_bit, st);
+  w.sort_tmp.ensure(tmp_bytes);
+  size_t eoff = 0;
+  for (int k = 0; k < nseg; k++) {
+    const uint32_t nk = segs[k].n;
+    if (!nk) continue;
+    const uint32_t nb = ceil_div(nk, 256);
+    const uint32_t kbase = p.shared ? (uint32_t)k << (p.segshift & 31) : 0u;
+    uint32_t* ki = w.key_in.as<uint32_t>() + eoff;
+    uint32_t* ei = w.ent_in.as<uint32_t>() + eoff;
+    if (sw == 1) k_msm_keys<1><<<nb, 256, 0, st>>>(segs[k].scalars, p, nk, nseg > 1 ? kbase : 0u, ki, ei);
+    else k_msm_keys<4><<<nb, 256, 0, st>>>(segs[k].scalars, p, nk, 0u, ki, ei);
     ZK_LAUNCH_CHECK();
-  } else {
-    // counting sort: global-atomic histogram, scan, scatter (single MSM)
-    const uint64_t* d_scalars = segs[0].scalars;
-    if (w.counts.bytes < sizeof(uint32_t) * (p.G + 1)) {   // zero once; k_scan_down re-zeroes
-      w.counts.ensure(sizeof(uint32_t) * (p.G + 1));
-      ZK_HIP(hipMemsetAsync(w.counts.p, 0, w.counts.bytes, st));
-    }
-    w.cursor.ensure(sizeof(uint32_t) * (p.G + 1));
-    w.scan_part.ensure(sizeof(uint32_t) * nblk);
-    if (n) {
-      const uint32_t nb = ceil_div(n, 256);
-      if (sw == 1)
-        k_msm_digits<1, false><<<nb, 256, 0, st>>>(d_scalars, p, w.counts.as<uint32_t>(), nullptr, nullptr, nullptr);
-      else
-        k_msm_digits<4, false><<<nb, 256, 0, st>>>(d_scalars, p, w.counts.as<uint32_t>(), nullptr, nullptr, nullptr);
-      ZK_LAUNCH_CHECK();
-    }
-    k_scan_local<<<nblk, 256, 0, st>>>(w.counts.as<uint32_t>(), p.G, w.scan_part.as<uint32_t>());
-    ZK_LAUNCH_CHECK();
-    k_scan_part<<<1, 1024, 0, st>>>(w.scan_part.as<uint32_t>(), nblk);
-    ZK_LAUNCH_CHECK();
-    k_scan_down<<<nblk, 256, 0, st>>>(w.counts.as<uint32_t>(), p.G, w.scan_part.as<uint32_t>(),
-                                      w.off.as<uint32_t>(), w.cursor.as<uint32_t>());
-    ZK_LAUNCH_CHECK();
-    if (n) {
-      const uint32_t nb = ceil_div(n, 256);
-      if (sw == 1)
-        k_msm_digits<1, true><<<nb, 256, 0, st>>>(d_scalars, p, nullptr, w.cursor.as<uint32_t>(),
-                                                  w.ent.as<uint32_t>(), w.key.as<uint32_t>());
-      else
-        k_msm_digits<4, true><<<nb, 256, 0, st>>>(d_scalars, p, nullptr, w.cursor.as<uint32_t>(),
-                                                  w.ent.as<uint32_t>(), w.key.as<uint32_t>());
-      ZK_LAUNCH_CHECK();
-    }
+    eoff += (size_t)nk * p.nwin;
   }
+  if (M)
+    sort_pairs_u32(w.sort_tmp.p, tmp_bytes, w.key_in.as<uint32_t>(), w.key.as<uint32_t>(), w.ent_in.as<uint32_t>(),
+                   w.ent.as<uint32_t>(), M, end_bit, st);
+  k_msm_offsets<<<ceil_div(M + 1, 256), 256, 0, st>>>(w.key.as<uint32_t>(), (uint32_t)M, p.G, w.off.as<uint32_t>());
+  ZK_LAUNCH_CHECK();
   if (pf) pf->end(st, ph);
-  if (w.sort_done) ZK_HIP(hipEventRecord(w.sort_done, st));   // the grouping is done
   // The number of non-zero digits M' <= M is known on device only: the T
   // accumulate threads split it evenly there (chunk_len), no host sync.
   if (M) {
-    // the accumulate may be held until another stream's event (the prove's
-    // quotient): its full-occupancy round would otherwise starve that work
-    if (w.accum_wait) ZK_HIP(hipStreamWaitEvent(st, w.accum_wait, 0));
     ph = pf ? pf->begin(st, (w.tag + (g2 ? "msm_accum_g2" : "msm_accum_g1")).c_str(), n) : -1;
-    // ZK_MSM_IDXMASK (experiment only, wrong results): confine the base
-    // gathers to a cache-resident prefix to measure the kernel without HBM
-    static const uint32_t idx_mask = [] {
-      const char* e = getenv("ZK_MSM_IDXMASK");
-      return e ? (uint32_t)strtoul(e, nullptr, 0) & 0x7fffffffu : 0x7fffffffu;
-    }();
-    bool pair = false, lazy = false;
-    if constexpr (std::is_same<C, G2>::value) {
-      pair = g2_pair_mode();
-      if (pair)
-        k_msm_accum_pair<<<ceil_div(2 * (size_t)p.T, 128), 128, 0, st>>>(
-            sb, p.segshift, idx_mask, w.ent.as<uint32_t>(), w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T,
-            w.buckets.as<X>(), w.partials.as<X>());
-    }
-    if constexpr (std::is_same<C, G1>::value) {
-      if (g1_lazy_mode()) {
-        lazy = true;
-        k_msm_accum_g1l<<<ceil_div(p.T, 128), 128, 0, st>>>(sb, p.segshift, idx_mask, w.ent.as<uint32_t>(),
-                                                             w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T,
-                                                             w.buckets.as<X>(), w.partials.as<X>());
-      }
-    }
-    if (!pair && !lazy)
-      k_msm_accum<C><<<ceil_div(p.T, 128), 128, 0, st>>>(sb, p.segshift, idx_mask, w.ent.as<uint32_t>(),
-                                                          w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T,
-                                                          w.buckets.as<X>(), w.partials.as<X>());
+    if constexpr (g2)
+      k_msm_accum_pair<<<ceil_div(2 * (size_t)p.T, 128), 128, 0, st>>>(sb, p.segshift, w.ent.as<uint32_t>(),
+                                                                        w.key.as<uint32_t>(), w.off.as<uint32_t>(),
+                                                                        p.G, p.T, w.buckets.as<X>(),
+                                                                        w.partials.as<X>());
+    else
+      k_msm_accum<C><<<ceil_div(p.T, 128), 128, 0, st>>>(sb, p.segshift, w.ent.as<uint32_t>(), w.key.as<uint32_t>(),
+                                                          w.off.as<uint32_t>(), p.G, p.T, w.buckets.as<X>(),
+                                                          w.partials.as<X>());
     ZK_LAUNCH_CHECK();
     if (pf) pf->end(st, ph);
   }
-  if (w.accum_done) ZK_HIP(hipEventRecord(w.accum_done, st));   // the next accumulate in a chain may start
   ph = pf ? pf->begin(st, (w.tag + "msm_merge").c_str(), p.G) : -1;   // buckets split across chunks
   w.nbig.ensure(sizeof(uint32_t));
   ZK_HIP(hipMemsetAsync(w.nbig.p, 0, sizeof(uint32_t), st));
-  if (g2 && g2_pair_mode())
+  if constexpr (g2)
     k_msm_fixup_pair<<<ceil_div(2 * (size_t)p.G, 128), 128, 0, st>>>(
         w.off.as<uint32_t>(), p.G, p.T, p.fix_max, w.nbig.as<uint32_t>(), reinterpret_cast<G2X*>(w.buckets.p),
         reinterpret_cast<const G2X*>(w.partials.p));
-  else if ((red_quad_mask() & 4) && !g2)
-    k_msm_fixup_q<C><<<ceil_div(4 * (size_t)p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), p.G, p.T, p.fix_max,
-                                                                     w.nbig.as<uint32_t>(), w.buckets.as<X>(),
-                                                                     w.partials.as<X>());
   else
     k_msm_fixup<C><<<ceil_div(p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), p.G, p.T, p.fix_max,
                                                         w.nbig.as<uint32_t>(), w.buckets.as<X>(), w.partials.as<X>());
@@ -1202,19 +879,16 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
   if (pf) pf->end(st, ph);
   ph = pf ? pf->begin(st, (w.tag + "msm_bucket_sum").c_str(), p.G) : -1;   // row/col sums + quantities
   constexpr int RW = ZK_RED_QWAVES;
-  if (g2 && g2_pair_mode())
+  if constexpr (g2)
     k_msm_rowcol_pair<<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(
         p, w.off.as<uint32_t>(), reinterpret_cast<const G2X*>(w.buckets.p), reinterpret_cast<G2X*>(w.rc.p));
-  else if ((red_quad_mask() & 2) || (!g2 && p.nrc <= rowcol_quad_max()))
+  else if (p.nrc <= ROWCOL_QUAD_MAX)
     k_msm_rowcol_q<C, RW><<<p.nrc, 64 * RW, 0, st>>>(p, w.off.as<uint32_t>(), w.buckets.as<X>(), w.rc.as<X>());
   else
     k_msm_rowcol<C><<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.off.as<uint32_t>(),
                                                                                   w.buckets.as<X>(), w.rc.as<X>());
   ZK_LAUNCH_CHECK();
-  if (red_quad_mask() & 1)
-    k_msm_quant_q<C, RW><<<p.nq, 64 * RW, 0, st>>>(p, w.rc.as<X>(), w.res.as<X>());
-  else
-    k_msm_quant<C><<<ceil_div(p.nq, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.rc.as<X>(), w.res.as<X>());
+  k_msm_quant_q<C, RW><<<p.nq, 64 * RW, 0, st>>>(p, w.rc.as<X>(), w.res.as<X>());
   ZK_LAUNCH_CHECK();
   if (pf) pf->end(st, ph);
 }
@@ -1330,18 +1004,10 @@ __global__ void __launch_bounds__(256) k_pad_copy(const uint4* __restrict__ in, 
   out[t] = k < iw ? in[i * iw + k] : make_uint4(0, 0, 0, 0);
 }
 
-static bool base_pad_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("ZK_BASE_PAD");
-    return !(e && std::strcmp(e, "0") == 0);
-  }();
-  return on;
-}
-
 template <class C>
 uint32_t msm_pad_bases(DevBuf& d, size_t n, hipStream_t st) {
   constexpr uint32_t sz = sizeof(typename C::A), padded = (sz + 127) / 128 * 128;
-  if (!base_pad_enabled() || padded == sz) return 0;
+  if (padded == sz) return 0;
   DevBuf out;
   out.ensure((size_t)padded * std::max<size_t>(n, 1));
   if (n) {

@@ -7,9 +7,9 @@
 // normalised affine output is bit-identical.
 //
 // Pipeline per MSM (one HIP stream; workspace reused across calls):
-//   1 digits   signed c-bit window digits -> bucket histogram (global atomics)
-//   2 scan     3-phase parallel exclusive scan -> bucket offsets
-//   3 scatter  (point index | sign) entries grouped by bucket (counting sort)
+//   1 keys     signed c-bit window digits -> one (bucket, point | sign) pair
+//              per (point, window)
+//   2 sort     rocPRIM radix sort of the pairs by bucket, then bucket offsets
 //   4 accum    the M non-zero digits split evenly over one full-occupancy
 //              round of threads, XYZZ += affine with run-length flush:
 //              load-balanced whatever the digit distribution
@@ -50,7 +50,6 @@ struct G2 {
 };
 
 constexpr int MSM_MAXWIN = 64;
-constexpr int MSM_SCAN_BLOCK = 1024;  // elements per scan block (256 threads x 4)
 
 struct MsmPlan {
   int c, nwin, bits, sw;            // window bits, #windows, scalar bits, u64 words/scalar
@@ -89,15 +88,12 @@ MsmPlan msm_make_plan_shared(uint32_t n, int bits, int sw, int c);
 
 // Device workspace of one in-flight MSM.
 struct MsmWork {
-  DevBuf counts, off, cursor, scan_part, ent, key, buckets, partials, partials2, rc, res;
-  DevBuf key_in, ent_in, sort_tmp;   // radix-sort path
+  DevBuf off, ent, key, buckets, partials, partials2, rc, res;
+  DevBuf key_in, ent_in, sort_tmp;   // radix-sort input and scratch
   DevBuf nbig;                       // buckets left to the merge levels
   PinnedBuf host_res;
   MsmPlan plan{};
   Prof* prof = nullptr;  // optional live kernel timing
-  hipEvent_t accum_wait = nullptr;   // if set, the accumulate kernel waits for this event
-  hipEvent_t sort_done = nullptr;    // if set, recorded once the entries are grouped by bucket
-  hipEvent_t accum_done = nullptr;   // if set, recorded once the accumulate kernel has run
   std::string tag;      // phase-name prefix (per-MSM profiling)
 };
 
@@ -124,8 +120,8 @@ void msm_precompute_windows(typename C::A* d_bases, size_t n, int W, int c, hipS
 // Base gathers by the accumulate are random: a packed 96-B G1 point straddles
 // two 128-B lines half the time (192-B G2: always 2-3 lines).  Padding each
 // point to whole lines (G1 128 B, G2 256 B) makes every gather exactly one
-// (two) line(s).  Returns the new stride in bytes, or 0 (packed) when
-// ZK_BASE_PAD=0; `d` is replaced by the padded copy of its n points.
+// (two) line(s).  Returns the new stride in bytes; `d` is replaced by the
+// padded copy of its n points.
 template <class C>
 uint32_t msm_pad_bases(DevBuf& d, size_t n, hipStream_t st);
 // XYZZ -> affine for n points with one Fermat inversion per 16-point chunk

@@ -127,7 +127,7 @@ struct PassIO {
   const Fr* stab;
   Fr scale;
   uint32_t flags;
-  uint64_t gmask = ~0ull;   // ZK_NTT_EXPMASK (experiment only, wrong results): confine HBM indices
+  uint32_t* chk = nullptr;   // first pass of an API transform: *chk |= 1 on a non-canonical input
 };
 
 // One pass = one four-step level.  The block of N = 2^(s_lo+ns) elements
@@ -163,8 +163,9 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(PassIO io, NttTabs tab
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) {
     const uint32_t r = k >> logC, c = k & (C - 1);
     const size_t gi = base + ((size_t)r << s_lo) + c;
-    const size_t si = (gather ? bitrev32((uint32_t)gi, log_n) : gi) & io.gmask;
+    const size_t si = gather ? bitrev32((uint32_t)gi, log_n) : gi;
     Fr v = ld_vec(&io.src[si]);
+    if (io.chk && !fr_lt_r(v)) atomicOr(io.chk, 1u);
     if (io.ltab) v = fp_mul(v, ld_vec(&io.ltab[si]));
     if (DIT && s_lo) v = fp_mul(v, tw_full(tabs, ((lo0 + c) * bitrev32(r, ns)) << tw_shift, log_n));
     st_vec(&sh[k], v);
@@ -173,7 +174,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(PassIO io, NttTabs tab
   ntt_rounds<DIT>(sh, tabs.sm, ns, logC);
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) {
     const uint32_t r = k >> logC, c = k & (C - 1);
-    const size_t go = (base + ((size_t)r << s_lo) + c) & io.gmask;
+    const size_t go = base + ((size_t)r << s_lo) + c;
     Fr v = ld_vec(&sh[k]);
     if (!DIT && s_lo) v = fp_mul(v, tw_full(tabs, ((lo0 + c) * bitrev32(r, ns)) << tw_shift, log_n));
     if (io.stab) v = fp_mul(v, ld_vec(&io.stab[go]));
@@ -182,14 +183,8 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(PassIO io, NttTabs tab
   }
 }
 
-static void run_pass_io(bool dit, const PassIO& io_in, const NttTabs& t, uint32_t log_n, uint32_t s_lo, uint32_t ns,
+static void run_pass_io(bool dit, const PassIO& io, const NttTabs& t, uint32_t log_n, uint32_t s_lo, uint32_t ns,
                         hipStream_t st) {
-  static const uint64_t gmask = [] {
-    const char* e = getenv("ZK_NTT_EXPMASK");
-    return e ? strtoull(e, nullptr, 0) : ~0ull;
-  }();
-  PassIO io = io_in;
-  io.gmask = gmask;
   const uint32_t logC = std::min<uint32_t>(s_lo, NTT_TILE_LOG - ns);
   const uint32_t tiles = (uint32_t)((1ull << log_n) >> (ns + logC));
   const size_t lds = sizeof(Fr) << (ns + logC);
@@ -207,17 +202,10 @@ static void run_pass(bool dit, Fr* d, const NttTabs& t, uint32_t log_n, uint32_t
 
 // Pass plan, top (first DIF pass) to bottom: the contiguous pass (s_lo = 0)
 // takes up to 11 stages; the rest are split evenly into strided passes of
-// <= ZK_NTT_MAXSTRIDED stages (default 11: at 2^22 two passes instead of
-// three, 0.580 vs 0.609 ms with depth 9, profiles/r02_ntt_sweep.txt; a
-// one-column tile's 32-byte rows share lines with its neighbours, which the
-// XCD-aware tile order keeps in one L2).
-static uint32_t max_strided() {
-  static const uint32_t v = [] {
-    const char* e = getenv("ZK_NTT_MAXSTRIDED");
-    return e ? (uint32_t)std::max(1, std::min(NTT_TILE_LOG, atoi(e))) : (uint32_t)NTT_TILE_LOG;
-  }();
-  return v;
-}
+// <= 11 stages (at 2^22 two passes instead of three: 0.580 vs 0.609 ms with
+// depth 9, profiles/r02_ntt_sweep.txt; a one-column tile's 32-byte rows share
+// lines with its neighbours, which the XCD-aware tile order keeps in one L2).
+static uint32_t max_strided() { return NTT_TILE_LOG; }
 static std::vector<uint32_t> pass_plan(uint32_t L) {
   const uint32_t last = std::min<uint32_t>(L, NTT_TILE_LOG);
   const uint32_t rest = L - last;
@@ -268,7 +256,7 @@ void ntt_dit(Fr* d, const NttDomain& dom, bool inv, hipStream_t st, Prof* pf) {
 // passes plus a bit reversal.  With more than one pass the intermediate
 // levels live in tmp (n elements), so src may equal dst.
 void ntt_natural(Fr* dst, const Fr* src, Fr* tmp, const NttDomain& dom, bool inv, hipStream_t st, Prof* pf,
-                 const Fr* ltab, const Fr* stab, const Fr* scale) {
+                 const Fr* ltab, const Fr* stab, const Fr* scale, uint32_t* chk) {
   const uint32_t L = dom.log_n;
   if (L == 0) return;
   const int ph = pf ? pf->begin(st, "ntt", (uint64_t)1 << L) : -1;
@@ -282,6 +270,7 @@ void ntt_natural(Fr* dst, const Fr* src, Fr* tmp, const NttDomain& dom, bool inv
     if (i == 0) {
       io.flags |= IO_GATHER;
       io.ltab = ltab;
+      io.chk = chk;
     }
     if (i + 1 == P) {
       io.stab = stab;
@@ -419,11 +408,7 @@ void ntt_domain_init(NttDomain& d, uint32_t log_n, hipStream_t st) {
   d.itl.ensure(sizeof(Fr) * ntl);
   d.th.ensure(sizeof(Fr) * nth);
   d.ith.ensure(sizeof(Fr) * nth);
-  d.gpow.ensure(sizeof(Fr) * n);
-  d.gipow.ensure(sizeof(Fr) * n);
-  d.gpow_br.ensure(sizeof(Fr) * n);
   Fr one = fr_const(FrParams::ONE);
-  Fr ninv = fr_const(FR_INV_2K[log_n]);
   fr_powers(d.sm.as<Fr>(), fr_const(FR_ROOTS[NTT_SM_LOG]), one, nsm, st);
   fr_powers(d.ism.as<Fr>(), fr_const(FR_ROOTS_INV[NTT_SM_LOG]), one, nsm, st);
   fr_powers(d.tl.as<Fr>(), fr_const(FR_ROOTS[log_n]), one, ntl, st);
@@ -432,12 +417,44 @@ void ntt_domain_init(NttDomain& d, uint32_t log_n, hipStream_t st) {
     fr_powers(d.th.as<Fr>(), fr_const(FR_ROOTS[log_n - NTT_TL_LOG]), one, nth, st);
     fr_powers(d.ith.as<Fr>(), fr_const(FR_ROOTS_INV[log_n - NTT_TL_LOG]), one, nth, st);
   }
-  fr_powers(d.gpow.as<Fr>(), fr_const(FR_GEN), ninv, n, st);
-  fr_powers(d.gipow.as<Fr>(), fr_const(FR_GEN_INV), ninv, n, st);
-  fr_bitrev_scale(d.gpow.as<Fr>(), d.gpow_br.as<Fr>(), log_n, nullptr, nullptr, st);
   d.zinv.ensure(sizeof(Fr));
   k_coset_zinv<<<1, 1, 0, st>>>(d.zinv.as<Fr>(), log_n);
   ZK_LAUNCH_CHECK();
+}
+
+const Fr* domain_gpow(NttDomain& d, hipStream_t st) {
+  if (!d.gpow.p) {
+    const size_t n = (size_t)1 << d.log_n;
+    d.gpow.ensure(sizeof(Fr) * n);
+    fr_powers(d.gpow.as<Fr>(), fr_const(FR_GEN), fr_const(FR_INV_2K[d.log_n]), n, st);
+  }
+  return d.gpow.as<Fr>();
+}
+
+const Fr* domain_gipow(NttDomain& d, hipStream_t st) {
+  if (!d.gipow.p) {
+    const size_t n = (size_t)1 << d.log_n;
+    d.gipow.ensure(sizeof(Fr) * n);
+    fr_powers(d.gipow.as<Fr>(), fr_const(FR_GEN_INV), fr_const(FR_INV_2K[d.log_n]), n, st);
+  }
+  return d.gipow.as<Fr>();
+}
+
+const Fr* domain_gpow_br(NttDomain& d, hipStream_t st) {
+  if (!d.gpow_br.p) {
+    const size_t n = (size_t)1 << d.log_n;
+    d.gpow_br.ensure(sizeof(Fr) * n);
+    if (d.gpow.p) {
+      fr_bitrev_scale(d.gpow.as<Fr>(), d.gpow_br.as<Fr>(), d.log_n, nullptr, nullptr, st);
+    } else {   // natural-order table only as scratch
+      DevBuf tmp;
+      tmp.ensure(sizeof(Fr) * n);
+      fr_powers(tmp.as<Fr>(), fr_const(FR_GEN), fr_const(FR_INV_2K[d.log_n]), n, st);
+      fr_bitrev_scale(tmp.as<Fr>(), d.gpow_br.as<Fr>(), d.log_n, nullptr, nullptr, st);
+      ZK_HIP(hipStreamSynchronize(st));   // tmp dies here
+    }
+  }
+  return d.gpow_br.as<Fr>();
 }
 
 // -------------------------------------------------------- elementwise ---

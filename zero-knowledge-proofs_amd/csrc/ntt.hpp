@@ -28,16 +28,30 @@ struct NttDomain {
   DevBuf sm, ism;   // omega_2048^j, j < 1024 (and inverse): sub-transform twiddles
   DevBuf tl, itl;   // omega_n^x, x < min(n, 4096)
   DevBuf th, ith;   // omega_n^(4096 y), y < n / 4096
+  DevBuf zinv;    // (g^n - 1)^-1: 1/Z on the coset g<w>
+  // n-entry coset tables, built on first use only (n x 32 B each: 512 MB at
+  // 2^24), so API-only transforms build none and each quotient path builds
+  // the ones it reads -- single GPU: gpow_br + gipow, distributed: gpow + gipow
   DevBuf gpow;    // n^-1 * g^i, i < n   (coset shift g = 7)
   DevBuf gpow_br; // gpow in bit-reversed order: read contiguously by the quotient's coset shift
   DevBuf gipow;   // n^-1 * g^-i, i < n
-  DevBuf zinv;    // (g^n - 1)^-1: 1/Z on the coset g<w>
 };
 
 void ntt_domain_init(NttDomain& d, uint32_t log_n, hipStream_t st);
+const Fr* domain_gpow(NttDomain& d, hipStream_t st);
+const Fr* domain_gpow_br(NttDomain& d, hipStream_t st);
+const Fr* domain_gipow(NttDomain& d, hipStream_t st);
 
 constexpr int NTT_SM_LOG = 11;    // sub-transform twiddles: powers of omega_2048 (domain-independent)
 constexpr int NTT_TL_LOG = 12;    // omega_n^x = TL[x mod 4096] * TH[x / 4096]
+
+// a (8 little-endian u32 limbs, as stored) < r: a canonical Fr
+ZK_DI bool fr_lt_r(const Fr& a) {
+  uint32_t br = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) (void)__builtin_subc(a.v[k], FrParams::MOD[k], br, &br);
+  return br != 0;   // a - r borrowed
+}
 
 ZK_DI uint32_t bitrev32(uint32_t x, uint32_t log_n) {
   return log_n ? (__builtin_bitreverse32(x) >> (32 - log_n)) : 0;
@@ -71,9 +85,10 @@ void ntt_dit(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_
 // Natural order in (src) and out (dst), the API transform: DIT passes whose
 // first pass gathers from bit-reversed positions; ltab: factor on the input
 // (natural index), stab / scale: factor on the output.  tmp: n elements of
-// scratch (src may equal dst).
+// scratch (src may equal dst).  chk: when given, *chk |= 1 if some input
+// element is not a canonical Fr (checked in the first pass's load).
 void ntt_natural(Fr* dst, const Fr* src, Fr* tmp, const NttDomain& dom, bool inverse_twiddles, hipStream_t st,
-                 Prof* pf, const Fr* ltab, const Fr* stab, const Fr* scale);
+                 Prof* pf, const Fr* ltab, const Fr* stab, const Fr* scale, uint32_t* chk = nullptr);
 
 // d <- NTT(tab_br[p] * iNTT(d)) with the inverse DIF's last pass, the
 // scale and the forward DIT's first pass fused into one tile kernel (the

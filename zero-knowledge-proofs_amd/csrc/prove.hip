@@ -146,11 +146,7 @@ __global__ void __launch_bounds__(256) k_check_canonical(const Fr* __restrict__ 
                                                          uint32_t* __restrict__ flags) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const Fr a = ld_vec(&z[i]);
-  uint32_t br = 0;
-#pragma unroll
-  for (int k = 0; k < 8; k++) (void)__builtin_subc(a.v[k], FrParams::MOD[k], br, &br);
-  if (!br) atomicOr(flags, 8u);   // a - r did not borrow: a >= r
+  if (!fr_lt_r(ld_vec(&z[i]))) atomicOr(flags, 8u);
 }
 
 void check_canonical(const void* d_z, uint64_t n, uint32_t* d_flags, hipStream_t st) {
@@ -206,32 +202,31 @@ static void pow64_chain(const host::X<typename C::HF>& P, ABI* out) {
   }
 }
 
-// Upload one base vector range [lo, hi): compact non-identity entries, append extras.
-// Positions lo, lo + stride, ... < hi (stride > 1: the H coefficients of a
-// shard, i = shard mod nshards, which is where the distributed quotient
-// leaves them).
-template <class C, class ABI>
+// Upload the non-identity entries at positions lo, lo + stride, ... < hi of
+// one base vector that `take` accepts, compacted, and append the extras.
+// stride > 1: the H coefficients of a shard, i = shard mod nshards, which is
+// where the distributed quotient leaves them.  The scalar of position i is
+// z_(i + idx_offset) (H: coefficient i).
+template <class C, class ABI, class Take>
 static void upload_vector(zk_pk_dev& pk, int slot, const ABI* v, uint64_t lo, uint64_t hi, uint64_t idx_offset,
-                          const std::vector<ABI>& extras, hipStream_t st, uint64_t stride = 1) {
-  std::vector<uint32_t> idx;
-  idx.reserve((hi - lo) / stride + 1);
+                          const std::vector<ABI>& extras, hipStream_t st, uint64_t stride, Take take) {
+  std::vector<uint32_t> gidx;
+  std::vector<ABI> pts;
   for (uint64_t i = lo; i < hi; i += stride)
-    if (!v[i].infinity) idx.push_back((uint32_t)(i - lo));
-  const uint32_t cnt = (uint32_t)idx.size();
+    if (!v[i].infinity && take(i)) {
+      gidx.push_back((uint32_t)(i + idx_offset));
+      pts.push_back(v[i]);
+    }
+  const uint32_t cnt = (uint32_t)gidx.size();
   const uint32_t nex = (uint32_t)extras.size();
   pk.count[slot] = cnt;
   pk.extras[slot] = nex;
   pk.bases[slot].ensure(sizeof(typename C::A) * std::max<uint64_t>(cnt + nex, 1));
   pk.idx[slot].ensure(sizeof(uint32_t) * std::max<uint32_t>(cnt, 1));
-  DevBuf raw, didx;
-  raw.ensure(sizeof(ABI) * std::max<uint64_t>(hi - lo, 1));
-  didx.ensure(sizeof(uint32_t) * std::max<uint32_t>(cnt, 1));
-  if (hi > lo) ZK_HIP(hipMemcpyAsync(raw.p, v + lo, sizeof(ABI) * (hi - lo), hipMemcpyHostToDevice, st));
-  if (cnt) ZK_HIP(hipMemcpyAsync(didx.p, idx.data(), sizeof(uint32_t) * cnt, hipMemcpyHostToDevice, st));
-  convert_bases_gather<C>(raw.as<uint64_t>(), didx.as<uint32_t>(), pk.bases[slot].as<typename C::A>(), cnt, st);
-  // scalar index = variable / coefficient index
-  std::vector<uint32_t> gidx(cnt);
-  for (uint32_t k = 0; k < cnt; k++) gidx[k] = (uint32_t)(idx[k] + lo + idx_offset);
+  DevBuf raw;
+  raw.ensure(sizeof(ABI) * std::max<uint64_t>(cnt, 1));
+  if (cnt) ZK_HIP(hipMemcpyAsync(raw.p, pts.data(), sizeof(ABI) * cnt, hipMemcpyHostToDevice, st));
+  convert_bases<C>(raw.as<uint64_t>(), pk.bases[slot].as<typename C::A>(), cnt, st);
   if (cnt) ZK_HIP(hipMemcpyAsync(pk.idx[slot].p, gidx.data(), sizeof(uint32_t) * cnt, hipMemcpyHostToDevice, st));
   if (nex) {
     DevBuf ex;
@@ -243,12 +238,26 @@ static void upload_vector(zk_pk_dev& pk, int slot, const ABI* v, uint64_t lo, ui
   ZK_HIP(hipStreamSynchronize(st));  // host vectors / staging die here
 }
 
+// Positions [0, L) of a base vector whose position i pairs with variable
+// i + off: this shard's variables (var_owner), or its contiguous range.
+template <class C, class ABI>
+static void vector_shard(zk_pk_dev& d, int slot, const ABI* v, uint64_t L, uint64_t off, const std::vector<ABI>& extras,
+                         const std::vector<uint8_t>& own, hipStream_t st) {
+  const uint32_t k = d.shard, N = d.nshards;
+  if (own.empty())
+    upload_vector<C>(d, slot, v, shard_lo(L, k, N), shard_lo(L, k + 1, N), off, extras, st, 1,
+                     [](uint64_t) { return true; });
+  else
+    upload_vector<C>(d, slot, v, 0, L, off, extras, st, 1, [&](uint64_t i) { return own[i + off] == k; });
+}
+
 zk_pk_dev* pk_upload(zk_ctx* ctx, const zk_pk* pk, const zk_r1cs_csr* q, uint32_t shard, uint32_t nshards) {
   hipStream_t st = ctx->stream;
   std::unique_ptr<zk_pk_dev> d(new zk_pk_dev());
   d->device = ctx->device;
   d->V = q->num_variables;
   d->nc = q->num_constraints;
+  if (d->nc > (1ull << 32)) throw Error(ZK_ERR_DOMAIN, "more than 2^32 constraints (Fr 2-adicity 32)");
   d->n = 1;
   while (d->n < d->nc) d->n <<= 1;
   d->log_n = (uint32_t)__builtin_ctzll(d->n);
@@ -271,36 +280,85 @@ zk_pk_dev* pk_upload(zk_ctx* ctx, const zk_pk* pk, const zk_r1cs_csr* q, uint32_
     exB1.push_back(pk->beta_g1);
   }
   const uint64_t V = d->V;
-  {
-    const uint64_t L = std::min<uint64_t>(pk->a_len, V);  // core:171 i < a_g1.len()
-    uint64_t lo = shard_lo(L, shard, nshards), hi = shard_lo(L, shard + 1, nshards);
-    upload_vector<G1>(*d, MSM_A, pk->a_g1, lo, hi, 0, exA, st);
-  }
-  {
-    const uint64_t L = std::min<uint64_t>(pk->b2_len, V);  // core:189
-    uint64_t lo = shard_lo(L, shard, nshards), hi = shard_lo(L, shard + 1, nshards);
-    upload_vector<G2>(*d, MSM_B2, pk->b_g2, lo, hi, 0, exB2, st);
-  }
-  {
-    const uint64_t L = std::min<uint64_t>(pk->b_len, V);  // core:250
-    uint64_t lo = shard_lo(L, shard, nshards), hi = shard_lo(L, shard + 1, nshards);
-    upload_vector<G1>(*d, MSM_B1, pk->b_g1, lo, hi, 0, exB1, st);
-  }
-  {
-    // ic_g1[k] pairs with variable k + num_public + 1 (core:227-231)
-    uint64_t L = std::min<uint64_t>(pk->ic_len, V > pk->num_public + 1 ? V - pk->num_public - 1 : 0);
-    uint64_t lo = shard_lo(L, shard, nshards), hi = shard_lo(L, shard + 1, nshards);
-    upload_vector<G1>(*d, MSM_IC, pk->ic_g1, lo, hi, pk->num_public + 1, none1, st);
-  }
+  const std::vector<uint8_t> own = var_owner(q, d->n, nshards);
+  vector_shard<G1>(*d, MSM_A, pk->a_g1, std::min<uint64_t>(pk->a_len, V), 0, exA, own, st);     // core:171
+  vector_shard<G2>(*d, MSM_B2, pk->b_g2, std::min<uint64_t>(pk->b2_len, V), 0, exB2, own, st);  // core:189
+  vector_shard<G1>(*d, MSM_B1, pk->b_g1, std::min<uint64_t>(pk->b_len, V), 0, exB1, own, st);   // core:250
+  // ic_g1[k] pairs with variable k + num_public + 1 (core:227-231)
+  vector_shard<G1>(*d, MSM_IC, pk->ic_g1,
+                   std::min<uint64_t>(pk->ic_len, V > pk->num_public + 1 ? V - pk->num_public - 1 : 0),
+                   pk->num_public + 1, none1, own, st);
   {
     // h_g1[i] pairs with H coefficient i (zip, core:211-215); H has n
     // coefficients; shard k takes i = k mod nshards
     uint64_t L = std::min<uint64_t>(pk->h_len, d->n);
-    upload_vector<G1>(*d, MSM_H, pk->h_g1, std::min<uint64_t>(shard, L), L, 0, none1, st, nshards);
+    upload_vector<G1>(*d, MSM_H, pk->h_g1, std::min<uint64_t>(shard, L), L, 0, none1, st, nshards,
+                      [](uint64_t) { return true; });
   }
   // the a/b vectors may be shorter than V (core:171 `i < pk.a_g1.len()`): indices stay < V.
   pk_precompute_windows(ctx, *d);
+  pk_witness_ranges(*d, q, st);
   return d.release();
+}
+
+std::vector<uint8_t> var_owner(const zk_r1cs_csr* q, uint64_t n, uint32_t N) {
+  std::vector<uint8_t> own;
+  if (N < 2 || !dist_quotient_ok(n, (int)N)) return own;
+  const uint64_t V = q->num_variables, nc = q->num_constraints, m = n / N, qq = m / N;
+  own.assign(V, 0xff);
+  const uint64_t* rps[3] = {q->a_rowptr, q->b_rowptr, q->c_rowptr};
+  const uint32_t* cols[3] = {q->a_col, q->b_col, q->c_col};
+  for (uint64_t j = 0; j < nc; j++) {   // rank of row j: its column b = j mod m lies in [rank q, rank q + q)
+    const uint8_t rk = (uint8_t)((j % m) / qq);
+    for (int mtx = 0; mtx < 3; mtx++)
+      for (uint64_t e = rps[mtx][j]; e < rps[mtx][j + 1]; e++) {
+        const uint32_t c = cols[mtx][e];
+        if (c < V && own[c] == 0xff) own[c] = rk;
+      }
+  }
+  for (uint64_t v = 0; v < V; v++)
+    if (own[v] == 0xff) own[v] = (uint8_t)(v * N / V);
+  return own;
+}
+
+// Exactly the z entries a shard reads when its quotient is distributed:
+// z_0 (the constant check, core:89-93), the variables behind its compacted
+// A / B2 / B1 / IC bases (the idx vectors) and the columns of the rows its
+// column slice evaluates (dist.hip stage A: rows a m + rank q + b', a < N,
+// b' < q).  Sorted, merged into ranges.
+void pk_witness_ranges(zk_pk_dev& pk, const zk_r1cs_csr* q, hipStream_t st) {
+  pk.wr_dist.clear();
+  if (pk.nshards < 2 || !dist_quotient_ok(pk.n, (int)pk.nshards)) return;
+  std::vector<uint32_t> vars;
+  for (int slot : {MSM_A, MSM_B2, MSM_B1, MSM_IC}) {
+    const size_t k = vars.size();
+    vars.resize(k + pk.count[slot]);
+    if (pk.count[slot])
+      ZK_HIP(hipMemcpyAsync(vars.data() + k, pk.idx[slot].p, sizeof(uint32_t) * pk.count[slot],
+                            hipMemcpyDeviceToHost, st));
+  }
+  ZK_HIP(hipStreamSynchronize(st));
+  vars.push_back(0);
+  const uint64_t N = pk.nshards, m = pk.n / N, qq = m / N;
+  const uint64_t* rps[3] = {q->a_rowptr, q->b_rowptr, q->c_rowptr};
+  const uint32_t* cols[3] = {q->a_col, q->b_col, q->c_col};
+  for (uint64_t a = 0; a < N; a++)
+    for (uint64_t b = 0; b < qq; b++) {
+      const uint64_t j = a * m + pk.shard * qq + b;
+      if (j >= pk.nc) continue;
+      for (int mtx = 0; mtx < 3; mtx++)
+        for (uint64_t e = rps[mtx][j]; e < rps[mtx][j + 1]; e++)
+          if (cols[mtx][e] < pk.V) vars.push_back(cols[mtx][e]);   // columns >= V are ignored (qap:122-124)
+    }
+  std::sort(vars.begin(), vars.end());
+  vars.erase(std::unique(vars.begin(), vars.end()), vars.end());
+  for (uint32_t v : vars) {
+    if (!pk.wr_dist.empty() && pk.wr_dist.back() == v) pk.wr_dist.back() = (uint64_t)v + 1;
+    else {
+      pk.wr_dist.push_back(v);
+      pk.wr_dist.push_back((uint64_t)v + 1);
+    }
+  }
 }
 
 // The prove MSMs all take 64-bit scalars (lo64, core:156-161 / 203-208, and
@@ -311,21 +369,14 @@ zk_pk_dev* pk_upload(zk_ctx* ctx, const zk_pk* pk, const zk_r1cs_csr* q, uint32_
 // accumulate adds against a 32x larger bucket reduction (~12 ms per proof).
 // Measured (window sweep): 2x slower at 2^20 constraints, 7 %
 // faster at 2^24 -- so 22 from 2^24 constraints per key shard up.
-// ZK_PROVE_WIN_C overrides (8..22).
-static int prove_win_c(const zk_pk_dev& pk) {
-  static const int env = [] {
-    const char* e = getenv("ZK_PROVE_WIN_C");
-    const int v = e ? atoi(e) : 0;
-    return v >= 8 && v <= 22 ? v : 0;
-  }();
-  if (env) return env;
+// zk_ctx_set_option(ZK_OPT_PROVE_WIN_C) forces 16 or 22 (tests).
+static int prove_win_c(const zk_ctx* ctx, const zk_pk_dev& pk) {
+  if (ctx->prove_win_c) return ctx->prove_win_c;
   return pk.n / std::max<uint64_t>(pk.nshards, 1) >= (1ull << 24) ? 22 : 16;
 }
 
 void pk_precompute_windows(zk_ctx* ctx, zk_pk_dev& pk) {
-  const char* e = getenv("ZK_MSM_PRECOMP");
-  if (e && std::strcmp(e, "0") == 0) return;
-  const int PROVE_WIN_C = prove_win_c(pk), PROVE_WIN = (64 + PROVE_WIN_C - 1) / PROVE_WIN_C;
+  const int PROVE_WIN_C = prove_win_c(ctx, pk), PROVE_WIN = (64 + PROVE_WIN_C - 1) / PROVE_WIN_C;
   hipStream_t st = ctx->stream;
   for (int slot = 0; slot < NUM_MSM; slot++) {
     const size_t n = (size_t)pk.count[slot] + pk.extras[slot];
@@ -384,24 +435,17 @@ static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipS
   // instead of a DIF plus an element-wise bit-reversed gather.  Same-box
   // A/B, overlapped prove: 2^24 fused 122.8 / separate 118.6 ms; 2^20 the
   // gather path 9.89 / natural 10.01 ms (profiles/r02_ab_quot.txt).
-  // ZK_NTT_FUSE=0/1 and ZK_H_NATURAL=0/1 force either choice.
+  // zk_ctx_set_option(ZK_OPT_QUOTIENT_PATH) forces either path (tests).
   constexpr uint32_t LARGE_Q_LOG = 23;
-  auto env_or = [](const char* name) {
-    const char* e = getenv(name);
-    return e ? (std::strcmp(e, "0") == 0 ? 0 : 1) : -1;
-  };
-  static const int fuse_env = env_or("ZK_NTT_FUSE"), nat_env = env_or("ZK_H_NATURAL");
-  const bool large = pk->log_n >= LARGE_Q_LOG;
-  const bool fuse = fuse_env >= 0 ? fuse_env == 1 : !large;
-  const bool natural = nat_env >= 0 ? nat_env == 1 : large;
+  const bool large = ctx->quot_path >= 0 ? ctx->quot_path == 1 : pk->log_n >= LARGE_Q_LOG;
   for (int k = 0; k < 3; k++) {
-    if (fuse) {
-      ntt_coset_shift(v[k], dom, dom.gpow_br.as<Fr>(), st, pf);
+    if (!large) {
+      ntt_coset_shift(v[k], dom, domain_gpow_br(dom, st), st, pf);
       continue;
     }
     ntt_dif(v[k], dom, /*inverse twiddles*/ true, st, pf);
     ph = pf->begin(st, "quotient_misc", n);
-    fr_scale_table(v[k], dom.gpow_br.as<Fr>(), pk->log_n, false, st);
+    fr_scale_table(v[k], domain_gpow_br(dom, st), pk->log_n, false, st);
     pf->end(st, ph);
     ntt_dit(v[k], dom, false, st, pf);
   }
@@ -416,20 +460,20 @@ static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipS
   // since beyond the MALL every gathered 32-B element was its own line/page
   ctx->scal[MSM_H].ensure(sizeof(uint64_t) * n);
   ctx->tmp_scal.ensure(sizeof(uint64_t) * n);
-  if (!natural) {
+  if (!large) {
     ntt_dif(v[0], dom, true, st, pf);
     ph = pf->begin(st, "quotient_misc", n);
-    k_h_final<<<ceil_div(n, 256), 256, 0, st>>>(v[0], dom.gipow.as<Fr>(), pk->log_n, ctx->tmp_scal.as<uint64_t>());
+    k_h_final<<<ceil_div(n, 256), 256, 0, st>>>(v[0], domain_gipow(dom, st), pk->log_n, ctx->tmp_scal.as<uint64_t>());
     ZK_LAUNCH_CHECK();
     pf->end(st, ph);
     return;
   }
   Fr* h = v[1];
   if (pk->log_n == 0) {   // a size-1 transform is the identity: only the factor
-    fr_scale_table(v[0], dom.gipow.as<Fr>(), 0, false, st);
+    fr_scale_table(v[0], domain_gipow(dom, st), 0, false, st);
     h = v[0];
   } else {
-    ntt_natural(v[1], v[0], v[2], dom, true, st, pf, nullptr, dom.gipow.as<Fr>(), nullptr);
+    ntt_natural(v[1], v[0], v[2], dom, true, st, pf, nullptr, domain_gipow(dom, st), nullptr);
   }
   ph = pf->begin(st, "quotient_misc", n);
   k_h_lo64<<<ceil_div(n, 256), 256, 0, st>>>(h, n, ctx->tmp_scal.as<uint64_t>());
@@ -437,65 +481,58 @@ static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipS
   pf->end(st, ph);
 }
 
-static bool dist_quotient_enabled() {
-  const char* e = getenv("ZK_DIST_QUOTIENT");
-  return !(e && std::strcmp(e, "0") == 0);
-}
-
-// A sharded key whose ctx is attached to the matching RCCL communicator
-// computes its quotient distributed (three all-to-alls per proof).
+// A sharded key whose ctx is attached to the matching exchange (an RCCL
+// communicator, or a host-staged one) computes its quotient distributed
+// (three all-to-alls per proof).
 static bool uses_dist_quotient(const zk_ctx* ctx, const zk_pk_dev* pk) {
   return pk->nshards > 1 && ctx->exch && ctx->exch->world == (int)pk->nshards &&
-         ctx->exch->rank == (int)pk->shard && dist_quotient_ok(pk->n, (int)pk->nshards) &&
-         dist_quotient_enabled();
+         ctx->exch->rank == (int)pk->shard && dist_quotient_ok(pk->n, (int)pk->nshards);
 }
+
+// The G1 MSMs run as two batches (msm_launch_batch: one sort, accumulate,
+// merge and bucket reduction per batch, so the latency-bound tails cost one
+// tree depth per batch): A, B1 and IC need only z and start with the
+// witness; H follows the quotient.
+static const int G1_ABI[3] = {MSM_A, MSM_B1, MSM_IC};
 
 // h_given (virtual-rank tests): this shard's lo64(H_(shard + nshards d)) is
 // already on the device, with the witness-check flags of all ranks.
+// ranges: only these [lo, hi) entries of d_z are valid (a witness slice),
+// else all of [0, V).
 static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, const zk_fr* r,
-                             const zk_fr* s, const uint64_t* h_given = nullptr, uint32_t given_flags = 0) {
+                             const zk_fr* s, const uint64_t* h_given = nullptr, uint32_t given_flags = 0,
+                             const std::vector<uint64_t>* ranges = nullptr) {
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
   const auto t_start = clk::now();
   hipStream_t st = ctx->stream;
   ctx->flags.ensure(16);
+  ctx->flags_host.ensure(16);
   ctx->prof.mark_origin(st);
   const int ph_span = ctx->prof.begin(st, "prove_gpu_span", pk->n);   // first kernel .. last MSM done
   ZK_HIP(hipMemsetAsync(ctx->flags.p, 0, 16, st));
-  check_canonical(d_z, pk->V, ctx->flags.as<uint32_t>(), st);   // every z_i < r, else ZK_ERR_ARG
-  // The five MSMs are independent.  Streams (<= GPU_MAX_HW_QUEUES = 4, so no
-  // two share a hardware queue): main (high priority) runs the quotient and
-  // then the H MSM that depends on it; side[0] (high priority) the G2 MSM,
-  // the longest chain; side[1] the IC MSM (3n bases); side[2] A then B1.
-  // Latency-bound phases (scan, bucket reduction) of one MSM overlap the
-  // throughput-bound accumulation of another.
-  ZK_HIP(hipEventRecord(ctx->ev_scal, st));           // z (and flags reset) ready
-  static const int sched_env = [] {
-    const char* e = getenv("ZK_PROVE_SCHED");
-    return e ? atoi(e) : 0;
-  }();
-  const int sched = ctx->sched >= 0 ? ctx->sched : sched_env;   // zk_ctx_set_schedule overrides
-  auto stream_of = [&](int slot) {
-    if (sched == 3) return st;   // fully serial (per-phase profiling)
-    return slot == MSM_H ? st : slot == MSM_B2 ? ctx->side[0] : slot == MSM_IC ? ctx->side[1] : ctx->side[2];
-  };
-  // The quotient: local (every coefficient), distributed over the RCCL
-  // ranks of a sharded key (this rank's coefficients i = shard mod N), or
-  // given (virtual-rank tests).
+  if (ranges) {   // every z_i < r, else ZK_ERR_ARG
+    for (size_t k = 0; k + 1 < ranges->size(); k += 2)
+      check_canonical(reinterpret_cast<const Fr*>(d_z) + (*ranges)[k], (*ranges)[k + 1] - (*ranges)[k],
+                      ctx->flags.as<uint32_t>(), st);
+  } else {
+    check_canonical(d_z, pk->V, ctx->flags.as<uint32_t>(), st);
+  }
+  ZK_HIP(hipEventRecord(ctx->ev_scal, st));                     // z (and flags reset) ready
+  // Streams (<= GPU_MAX_HW_QUEUES = 4, so no two share a hardware queue):
+  // main (high priority) runs the quotient and then the H batch that depends
+  // on it; side[0] (high) the G2 MSM, the longest chain; side[1] the A+B1+IC
+  // batch.  The latency-bound phases of one MSM overlap the throughput-bound
+  // accumulation of another.  Schedule 3 runs everything in order on main.
+  const bool serial = ctx->sched == 3;
+  hipStream_t s_g2 = serial ? st : ctx->side[0];
+  hipStream_t s_abi = serial ? st : ctx->side[1];
+  // The quotient: local (every coefficient), distributed over the ranks of
+  // a sharded key (this rank's coefficients i = shard mod N), or given
+  // (virtual-rank tests).
   const bool dist = !h_given && uses_dist_quotient(ctx, pk);
   const uint64_t* h_src = h_given ? h_given : ctx->tmp_scal.as<uint64_t>();
   const uint32_t h_div = (h_given || dist) ? pk->nshards : 1;
-  auto run_quotient = [&]() {
-    if (h_given) return;
-    if (dist) {
-      ctx->tmp_scal.ensure(sizeof(uint64_t) * (pk->n / pk->nshards));
-      h_src = ctx->tmp_scal.as<uint64_t>();
-      dist_quotient(ctx, pk, d_z, *ctx->exch, ctx->dq, ctx->flags.as<uint32_t>(), ctx->tmp_scal.as<uint64_t>(), st);
-    } else {
-      quotient(ctx, pk, d_z, st);   // (Az, Bz, Cz) -> lo64(H) in tmp_scal
-      h_src = ctx->tmp_scal.as<uint64_t>();
-    }
-  };
   // scalars of one MSM: lo64 of its variables (or H coefficients), then the
   // extras' scalars (1 for alpha_1 / beta_2 / beta_1, the u64 limbs of r or s)
   auto prep_scalars = [&](int slot, hipStream_t ss) {
@@ -518,227 +555,53 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       ZK_LAUNCH_CHECK();
     }
   };
-  auto launch_slot = [&](int slot, hipStream_t ss) {
-    prep_scalars(slot, ss);
-    const uint32_t n = pk->count[slot] + pk->extras[slot];
-    if (slot == MSM_B2) {
-      if (pk->win > 1)
-        msm_launch_shared<G2>(ctx->msm[slot], pk->bases[slot].as<G2A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64,
-                              pk->win_c, ss, pk->stride[slot]);
-      else
-        msm_launch<G2>(ctx->msm[slot], pk->bases[slot].as<G2A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64, ss,
-                       pk->stride[slot]);
-      msm_download<G2>(ctx->msm[slot], ss);
-    } else {
-      if (pk->win > 1)
-        msm_launch_shared<G1>(ctx->msm[slot], pk->bases[slot].as<G1A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64,
-                              pk->win_c, ss, pk->stride[slot]);
-      else
-        msm_launch<G1>(ctx->msm[slot], pk->bases[slot].as<G1A>(), ctx->scal[slot].as<uint64_t>(), 1, n, 64, ss,
-                       pk->stride[slot]);
-      msm_download<G1>(ctx->msm[slot], ss);
-    }
-  };
   static const char* const tags[NUM_MSM] = {"A/", "B2/", "B1/", "IC/", "H/"};
-  for (int slot = 0; slot < NUM_MSM; slot++) ctx->msm[slot].tag = sched == 3 ? tags[slot] : "";
-  // Batched G1 (default with window-shifted keys): the G1 MSMs run in groups,
-  // each group ONE msm_launch_batch (one sort, accumulate, merge and bucket
-  // reduction, so the latency-bound tails cost one tree depth per group) in
-  // the workspace of its first slot.  ZK_G1_GROUPS lists the groups, letters
-  // A (pi_A), B (B_1), I (IC), H (H), comma-separated; default "ABI,H": A, B1
-  // and IC start on side[1] with the witness, H follows the quotient on the
-  // main stream, the G2 MSM runs on side[0].  ZK_PROVE_SCHED: 0 G2 starts
-  // with the witness, 1 G2 waits for the quotient, 3 everything serial on
-  // main.  ZK_MSM_BATCH=0 keeps one MSM per slot on four streams (below).
-  static const bool batch_env = [] {
-    const char* e = getenv("ZK_MSM_BATCH");
-    return !(e && std::strcmp(e, "0") == 0);
-  }();
-  static const std::vector<std::vector<int>> groups = [] {
-    const char* e = getenv("ZK_G1_GROUPS");
-    std::string spec = e ? e : "ABI,H";
-    std::vector<std::vector<int>> g(1);
-    for (char ch : spec) {
-      if (ch == ',') { if (!g.back().empty()) g.emplace_back(); continue; }
-      const int slot = ch == 'A' ? MSM_A : ch == 'B' ? MSM_B1 : ch == 'I' ? MSM_IC : ch == 'H' ? MSM_H : -1;
-      if (slot >= 0) g.back().push_back(slot);
+  auto launch_batch = [&](const int* slots, int k, const char* tag, hipStream_t gs) {
+    MsmSeg segs[MSM_MAXSEG];
+    for (int i = 0; i < k; i++) {
+      prep_scalars(slots[i], gs);
+      segs[i] = MsmSeg{pk->bases[slots[i]].p, ctx->scal[slots[i]].as<uint64_t>(),
+                       pk->count[slots[i]] + pk->extras[slots[i]], pk->stride[slots[i]]};
     }
-    if (g.back().empty()) g.pop_back();
-    int seen = 0;
-    for (auto& grp : g) for (int sl : grp) seen |= 1 << sl;
-    if (seen != ((1 << MSM_A) | (1 << MSM_B1) | (1 << MSM_IC) | (1 << MSM_H)))
-      g = {{MSM_A, MSM_B1, MSM_IC}, {MSM_H}};
-    return g;
-  }();
-  const bool batch = batch_env && pk->win > 1;
-  std::vector<int> waits;   // slots whose ev_done the host tail waits for
-  if (batch) {
-    hipStream_t s2 = sched == 3 ? st : ctx->side[0];
-    auto launch_group = [&](const std::vector<int>& grp, hipStream_t gs) {
-      MsmSeg segs[MSM_MAXSEG];
-      for (size_t k = 0; k < grp.size(); k++) {
-        const int slot = grp[k];
-        prep_scalars(slot, gs);
-        segs[k] = MsmSeg{pk->bases[slot].p, ctx->scal[slot].as<uint64_t>(), pk->count[slot] + pk->extras[slot],
-                         pk->stride[slot]};
-      }
-      MsmWork& w = ctx->msm[grp[0]];
-      if (sched == 3) {
-        w.tag.clear();
-        for (int sl : grp) w.tag += tags[sl][0];
-        w.tag += "/";
-      }
-      msm_launch_batch<G1>(w, segs, (int)grp.size(), 64, pk->win_c, gs);
-      msm_download<G1>(w, gs);
-      ZK_HIP(hipEventRecord(ctx->ev_done[grp[0]], gs));
-      waits.push_back(grp[0]);
-    };
-    auto has_h = [](const std::vector<int>& grp) { return std::find(grp.begin(), grp.end(), (int)MSM_H) != grp.end(); };
-    // ZK_PROVE_SCHED=4: the quotient's kernels are queued first (host launch
-    // order only, no waits), then the G2 MSM and the groups.  5: the same,
-    // and the side streams' accumulate kernels wait for the quotient (their
-    // key and sort passes still overlap it): a full-occupancy accumulate
-    // round otherwise holds every SIMD's registers and starves the
-    // quotient's LDS-tiled NTT passes, which delays the H MSM behind it.
-    // 6: the H group's key and sort passes also go ahead (queued right
-    // after the quotient on the main stream) and every accumulate waits for
-    // them -- sorts and the quotient share the chip, the accumulates start
-    // together once every MSM's entries are grouped.  7: as 6, but the G2
-    // accumulate starts with the witness; only the batched G1 accumulates
-    // wait for the H group's sort.
-    for (int sl = 0; sl < NUM_MSM; sl++) {
-      ctx->msm[sl].accum_wait = nullptr;
-      ctx->msm[sl].sort_done = nullptr;
-      ctx->msm[sl].accum_done = nullptr;
+    MsmWork& w = ctx->msm[slots[0]];
+    w.tag = serial ? tag : "";
+    msm_launch_batch<G1>(w, segs, k, 64, pk->win_c, gs);
+    msm_download<G1>(w, gs);
+    ZK_HIP(hipEventRecord(ctx->ev_done[slots[0]], gs));
+  };
+  // G2 (pi_B), then A + B1 + IC, both starting with the witness
+  if (!serial) ZK_HIP(hipStreamWaitEvent(s_g2, ctx->ev_scal, 0));
+  {
+    MsmWork& w = ctx->msm[MSM_B2];
+    w.tag = serial ? tags[MSM_B2] : "";
+    prep_scalars(MSM_B2, s_g2);
+    msm_launch_shared<G2>(w, pk->bases[MSM_B2].as<G2A>(), ctx->scal[MSM_B2].as<uint64_t>(), 1,
+                          pk->count[MSM_B2] + pk->extras[MSM_B2], 64, pk->win_c, s_g2, pk->stride[MSM_B2]);
+    msm_download<G2>(w, s_g2);
+    ZK_HIP(hipEventRecord(ctx->ev_done[MSM_B2], s_g2));
+  }
+  if (!serial) ZK_HIP(hipStreamWaitEvent(s_abi, ctx->ev_scal, 0));
+  launch_batch(G1_ABI, 3, "ABI/", s_abi);
+  // the quotient, then H on the main stream
+  if (!h_given) {
+    if (dist) {
+      ctx->tmp_scal.ensure(sizeof(uint64_t) * (pk->n / pk->nshards));
+      h_src = ctx->tmp_scal.as<uint64_t>();
+      dist_quotient(ctx, pk, d_z, *ctx->exch, ctx->dq, ctx->flags.as<uint32_t>(), ctx->tmp_scal.as<uint64_t>(), st);
+    } else {
+      quotient(ctx, pk, d_z, st);   // (Az, Bz, Cz) -> lo64(H) in tmp_scal
+      h_src = ctx->tmp_scal.as<uint64_t>();
     }
-    if (sched >= 4 && sched <= 8) run_quotient();
-    // 8: the quotient first, then the accumulates one after another in
-    // ZK_ACCUM_ORDER ('H' the H group, '2' the G2 MSM, 'A' the other G1
-    // groups; default "H2A"): every sort still starts with the witness, and
-    // each MSM's latency-bound tail (merge, bucket sums) overlaps the next
-    // accumulate instead of three full-occupancy rounds fighting for the chip.
-    if (sched == 8) {
-      static const std::string order = [] {
-        const char* e = getenv("ZK_ACCUM_ORDER");
-        std::string o = e ? e : "H2A";
-        std::string s = o;
-        std::sort(s.begin(), s.end());
-        return s == "2AH" ? o : std::string("H2A");
-      }();
-      ZK_HIP(hipEventRecord(ctx->ev_quot, st));
-      ctx->flags_host.ensure(16);
-      ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
-      hipEvent_t prev = ctx->ev_quot;
-      int side = 1;
-      for (char u : order) {
-        if (u == '2') {
-          MsmWork& w = ctx->msm[MSM_B2];
-          w.accum_wait = prev;
-          w.accum_done = prev = ctx->ev_acc[MSM_B2];
-          ZK_HIP(hipStreamWaitEvent(s2, ctx->ev_scal, 0));
-          launch_slot(MSM_B2, s2);
-          continue;
-        }
-        for (const auto& grp : groups) {
-          if (has_h(grp) != (u == 'H')) continue;
-          MsmWork& w = ctx->msm[grp[0]];
-          w.accum_wait = (u == 'H' && prev == ctx->ev_quot) ? nullptr : prev;   // H: same stream as the quotient
-          w.accum_done = prev = ctx->ev_acc[grp[0]];
-          hipStream_t gs = st;
-          if (u != 'H') {
-            gs = ctx->side[side];
-            side = side + 1 < NUM_SIDE ? side + 1 : 1;
-            ZK_HIP(hipStreamWaitEvent(gs, ctx->ev_scal, 0));
-          }
-          launch_group(grp, gs);
-        }
-      }
-    }
-    if (sched == 5) {
-      ZK_HIP(hipEventRecord(ctx->ev_quot, st));
-      for (int sl = 0; sl < NUM_MSM; sl++) ctx->msm[sl].accum_wait = sl == MSM_H ? nullptr : ctx->ev_quot;
-    }
-    if (sched == 6 || sched == 7) {
-      ctx->flags_host.ensure(16);
-      ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
-      for (const auto& grp : groups)
-        if (has_h(grp)) {
-          ctx->msm[grp[0]].sort_done = ctx->ev_hsort;
-          launch_group(grp, st);
-        }
-      for (int sl = 0; sl < NUM_MSM; sl++) ctx->msm[sl].accum_wait = ctx->ev_hsort;
-      for (const auto& grp : groups)
-        if (has_h(grp)) ctx->msm[grp[0]].accum_wait = nullptr;
-      if (sched == 7) ctx->msm[MSM_B2].accum_wait = nullptr;
-    }
-    // the G2 MSM starts with the witness (ZK_PROVE_SCHED=1: after the quotient, below)
-    if (sched == 3) {
-      launch_slot(MSM_B2, st);
-    } else if (sched != 1 && sched != 8 && sched != 9) {
-      ZK_HIP(hipStreamWaitEvent(s2, ctx->ev_scal, 0));
-      launch_slot(MSM_B2, s2);
-    }
-    // groups without H start with the witness on side[1], side[2], ...
-    // 9: as 0, but the G2 accumulate waits until these groups' entries are
-    // sorted, so its full-occupancy round cannot starve their sorts (and
-    // with them the start of the largest accumulate).
-    int side = 1;
-    std::vector<hipStream_t> used;
-    hipEvent_t g1_sorted = nullptr;
-    for (const auto& grp : groups) {
-      if (has_h(grp) || sched == 8) continue;
-      hipStream_t gs = st;
-      if (sched != 3) {
-        gs = ctx->side[side];
-        side = side + 1 < NUM_SIDE ? side + 1 : 1;
-        ZK_HIP(hipStreamWaitEvent(gs, ctx->ev_scal, 0));
-        used.push_back(gs);
-      }
-      if (sched == 9) ctx->msm[grp[0]].sort_done = g1_sorted = ctx->ev_acc[grp[0]];
-      launch_group(grp, gs);
-    }
-    if (sched == 9) {
-      ZK_HIP(hipStreamWaitEvent(s2, ctx->ev_scal, 0));
-      ctx->msm[MSM_B2].accum_wait = g1_sorted;
-      launch_slot(MSM_B2, s2);
-    }
-    if (sched < 4 || sched > 8) run_quotient();
-    if (sched == 1) {
-      ZK_HIP(hipEventRecord(ctx->ev_quot, st));
-      ZK_HIP(hipStreamWaitEvent(s2, ctx->ev_quot, 0));
-      launch_slot(MSM_B2, s2);
-    }
-    ZK_HIP(hipEventRecord(ctx->ev_done[MSM_B2], s2));
-    waits.push_back(MSM_B2);
-    if (sched != 6 && sched != 7 && sched != 8) {
-      ctx->flags_host.ensure(16);
-      ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
-      for (const auto& grp : groups)
-        if (has_h(grp)) launch_group(grp, st);
-    }
-    if (ph_span >= 0) {
-      for (int sl : waits) ZK_HIP(hipStreamWaitEvent(st, ctx->ev_done[sl], 0));
-      ctx->prof.end(st, ph_span);
-    }
-  } else {
-    // ZK_PROVE_SCHED=3: everything on the main stream, in order, with per-MSM
-    // phase names.  Default: the four independent MSMs start on the side
-    // streams, the quotient and then H on the main one.
-    for (int k = 0; k < NUM_SIDE; k++) ZK_HIP(hipStreamWaitEvent(ctx->side[k], ctx->ev_scal, 0));
-    for (int slot : {MSM_B2, MSM_IC, MSM_A, MSM_B1}) {
-      launch_slot(slot, stream_of(slot));
-      ZK_HIP(hipEventRecord(ctx->ev_done[slot], stream_of(slot)));
-    }
-    run_quotient();
-    ctx->flags_host.ensure(16);
-    ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
-    launch_slot(MSM_H, st);
-    ZK_HIP(hipEventRecord(ctx->ev_done[MSM_H], st));
-    waits = {MSM_A, MSM_B2, MSM_B1, MSM_IC, MSM_H};
-    if (ph_span >= 0) {
-      for (int slot : {MSM_B2, MSM_IC, MSM_A, MSM_B1}) ZK_HIP(hipStreamWaitEvent(st, ctx->ev_done[slot], 0));
-      ctx->prof.end(st, ph_span);
-    }
+  }
+  ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
+  {
+    const int h_slot[1] = {MSM_H};
+    launch_batch(h_slot, 1, "H/", st);
+  }
+  const int waits[3] = {MSM_B2, MSM_A, MSM_H};   // MSM_A: the A+B1+IC batch
+  if (ph_span >= 0) {
+    for (int sl : waits) ZK_HIP(hipStreamWaitEvent(st, ctx->ev_done[sl], 0));
+    ctx->prof.end(st, ph_span);
   }
 
   // Host tails (Horner over each MSM's partials, then s A + r B1) run as
@@ -747,37 +610,34 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   ctx->prof.add_host("host_launch", ms_since(t_start));
   double t_fin = 0;
   Partial p{};
-  std::vector<bool> done(waits.size(), false);
-  bool sc_done = false, a_done = false, b1_done = false;
-  for (size_t left = waits.size(); left > 0;) {
+  bool done[3] = {false, false, false};
+  bool sc_done = false, ab_done = false;
+  for (int left = 3; left > 0;) {
+    // the H MSM waits for the peers' quotient stages: a dead peer must end
+    // this proof (ZK_ERR_RCCL, the exchange aborted) instead of hanging it
+    if (dist && (ctx->exch->async_error() || ms_since(t_start) > ctx->exch->timeout_ms))
+      throw Error(ZK_ERR_RCCL, "distributed quotient: a peer did not answer within the exchange timeout");
     bool progressed = false;
-    for (size_t wi = 0; wi < waits.size(); wi++) {
+    for (int wi = 0; wi < 3; wi++) {
       if (done[wi]) continue;
       const int slot = waits[wi];
       const hipError_t q = hipEventQuery(ctx->ev_done[slot]);
       if (q == hipErrorNotReady) continue;
       ZK_HIP(q);
       const auto t_f = clk::now();
-      auto take = [&](int sl, const host::X<host::Fq>& v) {
-        switch (sl) {
-          case MSM_A: p.A = v; a_done = true; break;
-          case MSM_B1: p.B1 = v; b1_done = true; break;
-          case MSM_IC: p.IC = v; break;
-          case MSM_H: p.H = v; break;
-        }
-      };
       if (slot == MSM_B2) {
         p.B2 = msm_finish<G2>(ctx->msm[slot]);
-      } else if (batch) {
-        for (const auto& grp : groups)
-          if (grp[0] == slot)
-            for (size_t k = 0; k < grp.size(); k++) take(grp[k], msm_finish_seg<G1>(ctx->msm[slot], (int)k));
+      } else if (slot == MSM_A) {
+        p.A = msm_finish_seg<G1>(ctx->msm[slot], 0);
+        p.B1 = msm_finish_seg<G1>(ctx->msm[slot], 1);
+        p.IC = msm_finish_seg<G1>(ctx->msm[slot], 2);
+        ab_done = true;
       } else {
-        take(slot, msm_finish<G1>(ctx->msm[slot]));
+        p.H = msm_finish_seg<G1>(ctx->msm[slot], 0);
       }
       done[wi] = progressed = true;
       left--;
-      if (!sc_done && a_done && b1_done) {
+      if (!sc_done && ab_done) {
         p.SC = host::mul2_scalar(p.A, s->l, p.B1, r->l);
         sc_done = true;
       }
@@ -788,11 +648,6 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   }
   for (int k = 0; k < NUM_SIDE; k++) ZK_HIP(hipStreamSynchronize(ctx->side[k]));
   ZK_HIP(hipStreamSynchronize(st));
-  for (int sl = 0; sl < NUM_MSM; sl++) {
-    ctx->msm[sl].accum_wait = nullptr;
-    ctx->msm[sl].sort_done = nullptr;
-    ctx->msm[sl].accum_done = nullptr;
-  }
   ctx->prof.add_host("host_finish", t_fin);
   ctx->prof.collect();
   const uint32_t flags = h_given ? given_flags : *ctx->flags_host.as<uint32_t>();
@@ -838,27 +693,102 @@ int prove_impl(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, size_t zlen, s
   return combine(&p, 1, out);
 }
 
-int prove_partial_impl(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, size_t zlen, size_t num_public,
-                       const zk_fr* r, const zk_fr* s, zk_prove_partial* out) {
+// z_host / ranges: a host witness slice (zk_groth16_prove_partial_host) to
+// upload first, after the ranks agreed, instead of the device witness d_z.
+static int prove_partial_common(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, const zk_fr* z_host,
+                                const std::vector<uint64_t>* ranges, size_t zlen, size_t num_public,
+                                const zk_fr* r, const zk_fr* s, zk_prove_partial* out) {
   std::memset(out, 0, sizeof *out);
   Partial p{};
   int local = ZK_OK;
   if (!fr_canonical(*r) || !fr_canonical(*s)) local = ZK_ERR_ARG;
   else if (num_public >= zlen || zlen != pk->V) local = ZK_ERR_INVALID_WITNESS;
-  // Ranks of a distributed quotient agree on the host-side checks before
-  // the first all-to-all: a rank that bailed out alone would leave its
-  // peers blocked in the collective.
-  if (uses_dist_quotient(ctx, pk)) {
-    const int agreed = ctx->exch->agree_max(local, ctx->stream);
-    if (local == ZK_OK) local = agreed;
+  const bool dist = uses_dist_quotient(ctx, pk);
+  if (dist && ctx->exch->broken) {
+    ctx->err = "the exchange was aborted by an earlier failed proof; attach a new one";
+    return ZK_ERR_RCCL;
   }
-  if (local != ZK_OK) {
-    p.status = local;
-  } else {
-    p = prove_partial(ctx, pk, reinterpret_cast<const uint64_t*>(d_z), r, s);
+  hipStream_t st = ctx->stream;
+  auto upload = [&]() {
+    if (!z_host) return;
+    ctx->z_canon.ensure(sizeof(zk_fr) * std::max<size_t>(pk->V, 1));
+    size_t off = 0;
+    for (size_t k = 0; k + 1 < ranges->size(); k += 2) {
+      const uint64_t lo = (*ranges)[k], len = (*ranges)[k + 1] - lo;
+      ZK_HIP(hipMemcpyAsync(static_cast<zk_fr*>(ctx->z_canon.p) + lo, z_host + off, sizeof(zk_fr) * len,
+                            hipMemcpyHostToDevice, st));
+      off += len;
+    }
+    d_z = ctx->z_canon.p;
+  };
+  if (!dist) {
+    if (local == ZK_OK) {
+      upload();
+      p = prove_partial(ctx, pk, reinterpret_cast<const uint64_t*>(d_z), r, s, nullptr, 0, ranges);
+    } else {
+      p.status = local;
+    }
+    std::memcpy(out->bytes, &p, sizeof p);
+    return p.status;
+  }
+  // Distributed quotient.  Every allocation it needs is made first, then
+  // the ranks agree on the host-side checks before the first all-to-all (a
+  // rank that bailed out alone would leave its peers blocked in the
+  // collective).  A failure after the agreement -- a transport error, a
+  // device error, a peer that stopped answering -- aborts the exchange, so
+  // the peers' pending transfers fail too, and marks it dead.
+  try {
+    if (local == ZK_OK) {
+      try {
+        dq_prepare(ctx, pk, (int)pk->nshards, ctx->dq, st);
+        ctx->tmp_scal.ensure(sizeof(uint64_t) * (pk->n / pk->nshards));
+        if (z_host) ctx->z_canon.ensure(sizeof(zk_fr) * std::max<size_t>(pk->V, 1));
+      } catch (const Error& e) {
+        local = e.code;
+        ctx->err = e.what();
+      }
+    }
+    const int agreed = ctx->exch->agree_max(local, st);
+    if (local == ZK_OK) local = agreed;
+    if (local != ZK_OK) {
+      p.status = local;
+    } else {
+      upload();
+      p = prove_partial(ctx, pk, reinterpret_cast<const uint64_t*>(d_z), r, s, nullptr, 0, ranges);
+    }
+  } catch (...) {
+    ctx->exch->broken = true;
+    ctx->exch->abort();
+    throw;
   }
   std::memcpy(out->bytes, &p, sizeof p);
   return p.status;
+}
+
+int prove_partial_impl(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, size_t zlen, size_t num_public,
+                       const zk_fr* r, const zk_fr* s, zk_prove_partial* out) {
+  return prove_partial_common(ctx, pk, d_z, nullptr, nullptr, zlen, num_public, r, s, out);
+}
+
+// The ranges a shard reads on this ctx: wr_dist with a distributed quotient,
+// else the whole witness.
+std::vector<uint64_t> witness_ranges(const zk_ctx* ctx, const zk_pk_dev* pk) {
+  if (uses_dist_quotient(ctx, pk)) return pk->wr_dist;
+  return {0, pk->V};
+}
+
+int prove_partial_host_impl(zk_ctx* ctx, const zk_pk_dev* pk, const zk_fr* z_slice, size_t slice_len, size_t zlen,
+                            size_t num_public, const zk_fr* r, const zk_fr* s, zk_prove_partial* out) {
+  const std::vector<uint64_t> ranges = witness_ranges(ctx, pk);
+  size_t want = 0;
+  for (size_t k = 0; k + 1 < ranges.size(); k += 2) want += ranges[k + 1] - ranges[k];
+  if (slice_len != want || (want && !z_slice)) {
+    std::memset(out, 0, sizeof *out);
+    ctx->err = "witness slice length " + std::to_string(slice_len) + " != " + std::to_string(want) +
+               " (zk_groth16_witness_ranges)";
+    return ZK_ERR_ARG;
+  }
+  return prove_partial_common(ctx, pk, nullptr, z_slice, &ranges, zlen, num_public, r, s, out);
 }
 
 // N virtual ranks of a sharded key on ONE device: the distributed quotient's

@@ -318,6 +318,7 @@ int setup_impl(zk_ctx* ctx, const zk_r1cs_csr* q, const zk_setup_params* P, uint
   // truncated copies (setup:155-159); the reference unwraps inverse(d~), inverse(g~)
   const uint64_t al = P->alpha.l[0], be = P->beta.l[0], ga = P->gamma.l[0], de = P->delta.l[0], ta = P->tau.l[0];
   if (de == 0 || ga == 0) return ZK_ERR_SETUP_PARAMS;
+  if (nc > (1ull << 32)) return ZK_ERR_DOMAIN;
   uint64_t n = 1;
   while (n < nc) n <<= 1;
   const uint32_t log_n = (uint32_t)__builtin_ctzll(n);
@@ -471,16 +472,19 @@ int setup_impl(zk_ctx* ctx, const zk_r1cs_csr* q, const zk_setup_params* P, uint
   ZK_HIP(hipMemcpyAsync(hh.data(), sh.p, 8 * n, hipMemcpyDeviceToHost, st));
   ZK_HIP(hipStreamSynchronize(st));
 
+  // this shard's variables (var_owner: those its quotient rows first read),
   // contiguous shard ranges, or (stride = nshards) positions i = shard mod nshards
+  const std::vector<uint8_t> own = var_owner(q, n, nshards);
   auto build_slot = [&](int slot, bool g2, const std::vector<uint64_t>& hs, const DevBuf& ds, uint64_t len,
                         uint64_t idx_offset, const std::vector<uint64_t>& extra_words, uint32_t nextra,
                         bool strided = false) {
-    const uint64_t lo = strided ? std::min<uint64_t>(shard, len) : len * shard / nshards;
-    const uint64_t hi = strided ? len : len * (shard + 1) / nshards;
+    const bool by_owner = !strided && !own.empty();
+    const uint64_t lo = strided ? std::min<uint64_t>(shard, len) : by_owner ? 0 : len * shard / nshards;
+    const uint64_t hi = strided || by_owner ? len : len * (shard + 1) / nshards;
     const uint64_t stride = strided ? nshards : 1;
     std::vector<uint32_t> loc, glob;
     for (uint64_t i = lo; i < hi; i += stride)
-      if (hs[i]) {
+      if (hs[i] && (!by_owner || own[i + idx_offset] == shard)) {
         loc.push_back((uint32_t)i);
         glob.push_back((uint32_t)(i + idx_offset));
       }
@@ -542,6 +546,7 @@ int setup_impl(zk_ctx* ctx, const zk_r1cs_csr* q, const zk_setup_params* P, uint
   build_slot(MSM_IC, false, hic, sic, nic, num_public + 1, none, 0);
   build_slot(MSM_H, false, hh, sh, n, 0, none, 0, /*strided*/ true);
   pk_precompute_windows(ctx, *d);
+  pk_witness_ranges(*d, q, st);
   *pk_dev = d.release();
   return ZK_OK;
 }
@@ -595,10 +600,10 @@ int qap_evaluate_impl(zk_ctx* ctx, const zk_r1cs_csr* q, const zk_fr* point, con
   if (!fr_canonical(*point)) return ZK_ERR_ARG;
   for (size_t i = 0; i < zlen; i++)
     if (!fr_canonical(z[i])) return ZK_ERR_ARG;
+  if (nc > (1ull << 32)) return ZK_ERR_DOMAIN;   // Fr 2-adicity 32 (qap:101-105); also keeps the loop finite
   uint64_t n = 1;
   while (n < nc) n <<= 1;
   const uint32_t log_n = (uint32_t)__builtin_ctzll(n);
-  if (log_n > 32) return ZK_ERR_DOMAIN;
   auto to_dev = [](const host::Fr& h) { Fr d; const host::Fr v = host::fr_to_dev(h); std::memcpy(d.v, v.l, 32); return d; };
   const host::Fr t = host::fr_to_mont(point->l);
   host::Fr tn = t;

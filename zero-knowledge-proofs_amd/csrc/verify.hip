@@ -116,10 +116,15 @@ bool is_zero6(const uint64_t* c) {
 
 // zcash / ark-bls12-381 0.4 compressed point, validated like
 // CanonicalDeserialize::deserialize_compressed (Validate::Yes): compression
-// flag set, infinity without the sort flag and with every x byte zero (the
-// zcash encoding has exactly one identity: anything else would make a
-// malleable proof encoding), x < p, x^3 + b a square, the flagged root, the
-// prime-order subgroup.
+// flag set, x < p, x^3 + b a square, the flagged root, the prime-order
+// subgroup.  One DELIBERATE DEVIATION from ark 0.4: an infinity encoding must
+// also have the sort flag clear and every x byte zero.  ark-bls12-381 0.4's
+// read_g1/g2_compressed returns the identity as soon as the infinity flag is
+// set without looking at the x bytes, so bytes it accepts (infinity with
+// stray x bits) are rejected here: the zcash encoding has exactly one
+// identity, and accepting others makes the proof encoding malleable.  The ark
+// source is not in the reference tree, so this behaviour is parity-unpinned
+// either way.
 static bool x_bytes_zero(const uint8_t* in, size_t len) {
   uint8_t acc = in[0] & 0x1f;   // flag bits masked off
   for (size_t i = 1; i < len; i++) acc |= in[i];

@@ -298,6 +298,7 @@ static int msm_dev(zk_ctx* ctx, const zk_msm_bases* b, const void* d_sc, size_t 
   if (n != b->n) return ZK_ERR_MSM_LEN;
   if (bits == 0 || bits > 256) return ZK_ERR_ARG;
   ZK_GUARD(ctx, {
+    Range range("zk_msm_dev");
     hipStream_t st = ctx->stream;
     const uint64_t* sc = reinterpret_cast<const uint64_t*>(d_sc);
     ctx->flags.ensure(16);
@@ -354,6 +355,7 @@ int zk_msm_g2_dev(zk_ctx* ctx, const zk_msm_bases* b, const void* d_sc, size_t n
 // a flag, read after the transform, turns into ZK_ERR_ARG (the data are then
 // unspecified).  The caller synchronises.
 static int ntt_device(zk_ctx* ctx, void* d_data, uint32_t log_n, int dir, const zk_fr* coset) {
+  Range range("zk_ntt");
   hipStream_t st = ctx->stream;
   const size_t n = (size_t)1 << log_n;
   if (coset && !fr_canonical(*coset)) return ZK_ERR_ARG;

@@ -1,6 +1,7 @@
 // common.hpp -- status codes, HIP error plumbing, device buffers.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <stdint.h>
 
 #include <cstdio>
@@ -83,6 +84,15 @@ struct PinnedBuf {
 };
 
 inline uint32_t ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+// roctx range on the host timeline around a phase's launches (rocprofv3
+// --marker-trace shows them beside the kernels; a no-op without a tracer).
+struct Range {
+  explicit Range(const char* what) { roctxRangePushA(what); }
+  ~Range() { roctxRangePop(); }
+  Range(const Range&) = delete;
+  Range& operator=(const Range&) = delete;
+};
 
 // Live kernel timing with HIP events on the launching stream (enabled by
 // zk_ctx_profile).  Each phase accumulates device time, launches and work

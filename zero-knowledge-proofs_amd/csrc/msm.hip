@@ -286,7 +286,7 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum(SegBases<typena
     }
     if (en == MSM_DUMMY) continue;   // zero digit (shared-bucket plans)
     // batch: bucket g >> segshift names the MSM whose bases entry en indexes
-    typename C::A a = ld_vec(seg_base(sb, g >> segshift, en));
+    typename C::A a = ld_vec(seg_base(sb, g >> segshift, en & 0x7fffffffu));
     if (en & 0x80000000u) a.y = f_neg(a.y);
     if (!aff_is_inf(a)) acc = xyzz_madd(acc, a);
   }
@@ -338,7 +338,7 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum_pair(SegBases<G
       run_start = e;
     }
     if (en == MSM_DUMMY) continue;
-    const Fq* bp = reinterpret_cast<const Fq*>(seg_base(sb, g >> segshift, en)) + h;
+    const Fq* bp = reinterpret_cast<const Fq*>(seg_base(sb, g >> segshift, en & 0x7fffffffu)) + h;
     Affine<Fq2h> a{{ld_vec(bp)}, {ld_vec(bp + 2)}};
     if (en & 0x80000000u) a.y = f_neg(a.y);
     if (!aff_is_inf(a)) acc = xyzz_madd(acc, a);

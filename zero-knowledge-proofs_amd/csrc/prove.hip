@@ -505,6 +505,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
   const auto t_start = clk::now();
+  Range range_prove("zk_prove");
   hipStream_t st = ctx->stream;
   ctx->flags.ensure(16);
   ctx->flags_host.ensure(16);
@@ -557,6 +558,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   };
   static const char* const tags[NUM_MSM] = {"A/", "B2/", "B1/", "IC/", "H/"};
   auto launch_batch = [&](const int* slots, int k, const char* tag, hipStream_t gs) {
+    Range range(k == 1 ? "msm_g1_h" : "msm_g1_a_b1_ic");
     MsmSeg segs[MSM_MAXSEG];
     for (int i = 0; i < k; i++) {
       prep_scalars(slots[i], gs);
@@ -572,6 +574,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   // G2 (pi_B), then A + B1 + IC, both starting with the witness
   if (!serial) ZK_HIP(hipStreamWaitEvent(s_g2, ctx->ev_scal, 0));
   {
+    Range range("msm_g2");
     MsmWork& w = ctx->msm[MSM_B2];
     w.tag = serial ? tags[MSM_B2] : "";
     prep_scalars(MSM_B2, s_g2);
@@ -584,6 +587,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   launch_batch(G1_ABI, 3, "ABI/", s_abi);
   // the quotient, then H on the main stream
   if (!h_given) {
+    Range range(dist ? "quotient_distributed" : "quotient");
     if (dist) {
       ctx->tmp_scal.ensure(sizeof(uint64_t) * (pk->n / pk->nshards));
       h_src = ctx->tmp_scal.as<uint64_t>();
@@ -608,6 +612,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   // each MSM's stream reaches its event, overlapping the MSMs still on the
   // GPU.
   ctx->prof.add_host("host_launch", ms_since(t_start));
+  Range range_tail("host_tail");
   double t_fin = 0;
   Partial p{};
   bool done[3] = {false, false, false};

@@ -309,6 +309,7 @@ static void csr_to_csc(uint64_t nc, uint64_t V, const uint64_t* rp, const uint32
 // ---------------------------------------------------------------- setup ---
 int setup_impl(zk_ctx* ctx, const zk_r1cs_csr* q, const zk_setup_params* P, uint64_t num_public, uint32_t shard,
                uint32_t nshards, zk_pk* pk_host, zk_pk_dev** pk_dev, zk_vk* vk) {
+  Range range("zk_setup");
   hipStream_t st = ctx->stream;
   const uint64_t V = q->num_variables, nc = q->num_constraints;
   // SetupParams::validate (setup:128-136) and num_public < V (setup:148-152)

@@ -151,6 +151,36 @@ def roofline_from(prof, log_n, overlapped=None):
     return out
 
 
+def host_threads_label(nt):
+    """Which host cores a CPU leg used: OMP threads against the lease's
+    affinity set and the CPUs the OS shows (a GPU box lease sees far more
+    CPUs than it may use)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    what = "all cores of this lease" if nt == aff else f"{nt} of the lease's {aff} affinity CPUs (OMP_NUM_THREADS)"
+    return {"threads": nt, "affinity_cpus": aff, "host_cpus_visible": os.cpu_count(), "label": what}
+
+
+def oracle_threads():
+    """The oracle's default OpenMP thread count (oracle/binding.py)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import binding as oracle   # cpu_baseline legs only
+    return oracle.default_threads()
+
+
+def oracle_leg(fn, threads):
+    """Time fn() with the oracle on `threads` OpenMP threads."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import binding as oracle   # cpu_baseline legs only
+    prev = oracle.get_threads()
+    oracle.set_threads(threads)
+    try:
+        t0 = time.perf_counter()
+        out = fn(oracle)
+        return out, time.perf_counter() - t0
+    finally:
+        oracle.set_threads(prev)
+
+
 def host_cpu():
     model = platform.processor() or ""
     try:
@@ -217,11 +247,12 @@ def cpu_baseline(zkp, ctx, n, params, r, s, z_host, gpu_proof, log_n_1t, seed):
     g1 = zkp.Prover.prove(dpk1, zkp.Witness(z1, 1), r=r, s=s)
     dpk1.free()
     cpu = host_cpu()
+    lab = host_threads_label(nt)
     return {"value": round(n / dt_all, 2), "unit": "constraints/s", "cores": nt, "kind": "port",
             "sample": f"oracle/zk_oracle.c prove() of the full 2^{n.bit_length() - 1}-constraint circuit on "
-                      f"{nt} threads (OpenMP: MSM point chunks, FFT butterflies), {dt_all:.2f} s, same pk/z/r/s "
+                      f"{lab['label']} (OpenMP: MSM point chunks, FFT butterflies), {dt_all:.2f} s, same pk/z/r/s "
                       f"as the GPU's timed proof",
-            "cpu_model": cpu, "host_cpus_visible": os.cpu_count(),
+            "cpu_model": cpu, "host_cpus_visible": os.cpu_count(), "affinity_cpus": lab["affinity_cpus"],
             "bit_exact_vs_gpu": exact,
             "single_thread": {"value": round(n1 / dt_1, 2), "unit": "constraints/s", "cores": 1,
                               "sample": f"2^{log_n_1t}-constraint prove, 1 thread (the reference's build), "
@@ -229,7 +260,22 @@ def cpu_baseline(zkp, ctx, n, params, r, s, z_host, gpu_proof, log_n_1t, seed):
                               "bit_exact_vs_gpu": bool(np.array_equal(g1.words, proof1))}}
 
 
-def msm_g1_bench(zkp, ctx, log_n, steps, warmup, seed):
+FR_MUL_MADS = 9 * 9 * 2   # radix-2^29 Fr product: 81 limb products + 81 in the reduction (ff.hpp)
+
+
+def traffic_file(name):
+    """HBM bytes per launch of a kernel from a committed rocprofv3 FETCH/WRITE
+    pass (profiles/<name>), else (None, None)."""
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None, None
+    try:
+        return json.load(open(path)).get("bytes_per_launch"), os.path.relpath(path, ROOT)
+    except Exception:
+        return None, None
+
+
+def msm_g1_bench(zkp, ctx, log_n, steps, warmup, seed, cpu=True):
     """configs[1]: G1 MSM, 2^log_n bases, uniform full-width scalars, inputs in HBM."""
     import ctypes as C
     import torch
@@ -247,8 +293,9 @@ def msm_g1_bench(zkp, ctx, log_n, steps, warmup, seed):
     sc64 = np.zeros_like(sc)                 # also the prove path's 64-bit scalars
     sc64[:, 0] = sc[:, 0]
     d_sc64 = torch.from_numpy(sc64.view(np.int64)).to(f"cuda:{ctx.device}")
+    phases = {}
 
-    def measure(windows, bits=255):
+    def measure(windows, bits=255, profile=False):
         """windows: bases uploaded with their window-shifted copies (13 at c = 20 for 255-bit scalars,
         4 at c = 16 for 64-bit ones; zk_msm_g1_upload_windows: one bucket set), else plain."""
         hb = C.c_void_p()
@@ -271,10 +318,16 @@ def msm_g1_bench(zkp, ctx, log_n, steps, warmup, seed):
             run()
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / steps
+        if profile:   # per-phase kernel time from live HIP events, untimed loop
+            ctx.profile(True)
+            for _ in range(steps):
+                run()
+            phases.update(ctx.profile_read())
+            ctx.profile(False)
         zkp.lib().zk_msm_bases_free(hb)
         return dt, t_up, out.copy()
 
-    dt, t_up, r1 = measure(True)
+    dt, t_up, r1 = measure(True, profile=True)
     dt_plain, _, r2 = measure(False)
     if not np.array_equal(r1, r2):
         raise SystemExit("windowed and plain MSM disagree")
@@ -282,18 +335,56 @@ def msm_g1_bench(zkp, ctx, log_n, steps, warmup, seed):
     dt64_plain, _, r4 = measure(False, 64)
     if not np.array_equal(r3, r4):
         raise SystemExit("windowed and plain 64-bit MSM disagree")
-    return {"pairs_per_s": round(n / dt, 1), "n": n, "scalar_bits": 255, "ms_per_msm": round(dt * 1e3, 3),
-            "bases": "uploaded once with 13 window-shifted copies (c = 20; zk_msm_g1_upload_windows, %.0f ms)" % (t_up * 1e3),
-            "plain": {"pairs_per_s": round(n / dt_plain, 1), "ms_per_msm": round(dt_plain * 1e3, 3),
-                      "bases": "uploaded once, one copy (zk_msm_g1_upload)"},
-            "bits64": {"pairs_per_s": round(n / dt64, 1), "ms_per_msm": round(dt64 * 1e3, 3),
-                       "plain_ms_per_msm": round(dt64_plain * 1e3, 3),
-                       "note": "the same bases with the low 64 bits of the scalars (the prove path's lo64 "
-                               "distribution): 4 window copies at c = 16; checked equal to the plain upload"},
-            "parity": "tests/test_gpu_headline.py::test_msm_g1_2p20_closed_form (same sizes, closed form)"}
+    # roofline: the whole MSM and its dominant kernel (the bucket accumulate),
+    # 128 B per pair; VALU at 3542 v_mad per mixed add, one add
+    # per (point, digit window): 13 windows of 20 bits for 255-bit scalars
+    nwin = -(-255 // 20)
+    ph = {k: v["ms"] / steps for k, v in phases.items() if k.startswith("msm_")}
+    tot = sum(ph.values()) or float("nan")
+    acc_ms = ph.get("msm_accum_g1", float("nan"))
+    algo = G1_PAIR_BYTES * n
+    tmads = n * nwin * MADS_PER_MADD / (acc_ms / 1e3) / 1e12
+    traffic, tsrc = traffic_file(f"pmc_msm_2p{log_n}.json")
+    roof = {"bound": "hbm", "achieved": round(algo / dt / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(algo / dt / 1e9 / HBM_PEAK_GBS, 6), "traffic": traffic, "traffic_source": tsrc,
+            "algorithmic_bytes": algo, "kernel": "k_msm_accum<G1>", "kernel_ms": round(acc_ms, 4),
+            "kernel_frac": round(algo / (acc_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 6),
+            "valu": {"achieved_tmad_per_s": round(tmads, 2), "peak_tmad_per_s": VALU_PEAK_TMADS,
+                     "frac": round(tmads / VALU_PEAK_TMADS, 4),
+                     "count": f"{nwin} windows x n mixed adds x {MADS_PER_MADD} v_mad_u64_u32, accumulate kernel"},
+            "phase_ms": {k: round(v, 4) for k, v in ph.items()},
+            "sort_and_reduction_share": round(1 - acc_ms / tot, 4),
+            "note": "integer-VALU bound (381-bit Montgomery products); HBM frac reported as north_star asks"}
+    rec = {"pairs_per_s": round(n / dt, 1), "n": n, "scalar_bits": 255, "ms_per_msm": round(dt * 1e3, 3),
+           "bases": "uploaded once with 13 window-shifted copies (c = 20; zk_msm_g1_upload_windows, %.0f ms)" % (t_up * 1e3),
+           "plain": {"pairs_per_s": round(n / dt_plain, 1), "ms_per_msm": round(dt_plain * 1e3, 3),
+                     "bases": "uploaded once, one copy (zk_msm_g1_upload)"},
+           "bits64": {"pairs_per_s": round(n / dt64, 1), "ms_per_msm": round(dt64 * 1e3, 3),
+                      "plain_ms_per_msm": round(dt64_plain * 1e3, 3),
+                      "note": "the same bases with the low 64 bits of the scalars (the prove path's lo64 "
+                              "distribution): 4 window copies at c = 16; checked equal to the plain upload"},
+           "roofline": roof,
+           "parity": "tests/test_gpu_headline.py::test_msm_g1_2p20_closed_form (same sizes, closed form)"}
+    if cpu:
+        # the oracle's ark-style signed-digit Pippenger on the same bases and
+        # scalars: all OMP threads on the full size (checked equal to the GPU
+        # result), one thread on a 2^16 prefix
+        nt = oracle_threads()
+        res, dt_n = oracle_leg(lambda o: o.msm_g1(bases, sc), nt)
+        n1 = min(n, 1 << 16)
+        _, dt_1 = oracle_leg(lambda o: o.msm_g1(bases[:n1], sc[:n1]), 1)
+        lab = host_threads_label(nt)
+        rec["cpu_baseline"] = {"value": round(n / dt_n, 1), "unit": "pairs/s", "cores": nt, "kind": "port",
+                               "sample": f"oracle/zk_oracle.c or_msm_g1 (ark-style signed-digit Pippenger), the "
+                                         f"same 2^{log_n} bases and scalars on {lab['label']}, {dt_n:.2f} s",
+                               "bit_exact_vs_gpu": bool(np.array_equal(res, r1)), **{k: lab[k] for k in
+                                                                                       ("affinity_cpus", "host_cpus_visible")},
+                               "single_thread": {"value": round(n1 / dt_1, 1), "unit": "pairs/s", "cores": 1,
+                                                 "sample": f"2^{n1.bit_length() - 1}-pair prefix, 1 thread, {dt_1:.2f} s"}}
+    return rec
 
 
-def ntt_bench(zkp, ctx, log_n, steps, warmup, seed):
+def ntt_bench(zkp, ctx, log_n, steps, warmup, seed, cpu=True):
     """configs[2]: forward radix-2 NTT over Fr, 2^log_n points in HBM, plus a
     round-trip check (inverse of the forward is the identity)."""
     import ctypes as C
@@ -320,18 +411,52 @@ def ntt_bench(zkp, ctx, log_n, steps, warmup, seed):
     for _ in range(steps):
         run(-1)
     ok = bool(np.array_equal(d.cpu().numpy().view(np.uint64).reshape(-1, 4), x))
-    ctx.profile(True)            # kernel time from the live HIP events, in a separate (untimed) loop
-    run(1)
-    run(-1)
+    # kernel time of the forward transform alone: HIP events around its
+    # passes on the launching stream, over the same number of forward calls
+    ctx.profile(True)
+    for _ in range(steps):
+        run(1)
     torch.cuda.synchronize()
-    prof = ctx.profile_read()
+    k = ctx.profile_read().get("ntt", {"ms": 0.0, "launches": 0})
     ctx.profile(False)
-    steps = 2
-    k = prof.get("ntt", {"ms": 0.0, "launches": 0})
-    return {"log_n": log_n, "ms_per_ntt": round(dt * 1e3, 3), "elements_per_s": round(n / dt, 1),
-            "kernel_ms_per_ntt": round(k["ms"] / max(steps, 1), 4),
-            "api": "zk_ntt_fr_dev (natural order in and out, data in HBM, one stream sync per call)",
-            "roundtrip_identity": ok}
+    y = d.cpu().numpy().view(np.uint64).reshape(-1, 4).copy()   # = NTT^steps(x): only the roofline run's state
+    kms = k["ms"] / max(k["launches"], 1)
+    algo = 2 * 32 * n
+    bfly = (n // 2) * log_n
+    tmads = bfly * FR_MUL_MADS / (kms / 1e3) / 1e12
+    traffic, tsrc = traffic_file(f"pmc_ntt_2p{log_n}.json")
+    rec = {"log_n": log_n, "ms_per_ntt": round(dt * 1e3, 3), "elements_per_s": round(n / dt, 1),
+           "kernel_ms_per_ntt": round(kms, 4),
+           "kernel_timing": "HIP events around the forward transform's passes on its stream, %d calls" % steps,
+           "api": "zk_ntt_fr_dev (natural order in and out, data in HBM, one stream sync per call)",
+           "roundtrip_identity": ok,
+           "roofline": {"bound": "hbm", "achieved": round(algo / (kms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, 6),
+                        "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes": algo,
+                        "valu": {"achieved_tmad_per_s": round(tmads, 2), "peak_tmad_per_s": VALU_PEAK_TMADS,
+                                 "frac": round(tmads / VALU_PEAK_TMADS, 4),
+                                 "count": f"(n/2) log n butterflies x {FR_MUL_MADS} v_mad (one Fr product each)"},
+                        "note": "latency-bound inside the butterfly chains (DESIGN.md 7.3)"}}
+    if cpu:
+        # the oracle's radix-2 FFT (ark-poly Radix2EvaluationDomain semantics)
+        # on the same input, all OMP threads, then one thread; both checked
+        # against a GPU forward transform of the same input
+        d.copy_(torch.from_numpy(x.view(np.int64).copy()).to(d.device))
+        run(1)
+        gpu_y = d.cpu().numpy().view(np.uint64).reshape(-1, 4).copy()
+        nt = oracle_threads()
+        yn, dt_n = oracle_leg(lambda o: o.fft(x), nt)
+        y1, dt_1 = oracle_leg(lambda o: o.fft(x), 1)
+        lab = host_threads_label(nt)
+        rec["cpu_baseline"] = {"value": round(n / dt_n, 1), "unit": "elements/s", "cores": nt, "kind": "port",
+                               "sample": f"oracle/zk_oracle.c or_fft (iterative radix-2, ark-poly semantics), the same "
+                                         f"2^{log_n} input on {lab['label']}, {dt_n:.2f} s",
+                               "bit_exact_vs_gpu": bool(np.array_equal(yn, gpu_y) and np.array_equal(y1, gpu_y)),
+                               "affinity_cpus": lab["affinity_cpus"], "host_cpus_visible": lab["host_cpus_visible"],
+                               "single_thread": {"value": round(n / dt_1, 1), "unit": "elements/s", "cores": 1,
+                                                 "sample": f"the full 2^{log_n} transform, 1 thread, {dt_1:.2f} s"}}
+    del y
+    return rec
 
 
 def main():
@@ -406,7 +531,8 @@ def main():
         # configs[2] first, on a fresh context (after the prove's multi-GB key
         # allocations the same transform measured ~20 % slower)
         log("[bench] NTT 2^22 (configs[2])")
-        extra["ntt"] = ntt_bench(zkp, ctx, 22, args.steps, args.warmup, args.seed + 31)
+        extra["ntt"] = ntt_bench(zkp, ctx, 22, args.steps, args.warmup, args.seed + 31,
+                                 cpu=not args.no_cpu_baseline)
     log(f"[bench] setup 2^{log_n_total}-constraint synthetic circuit on GPU (shard {rank}/{world})")
     qap = zkp.QAP(zkp.CSRMatrices.synthetic(n))
     t0 = time.perf_counter()
@@ -496,7 +622,7 @@ def main():
             t_ser = (time.perf_counter() - t0) / ks
             serial_prof = ctx.profile_read()
             ctx.profile(False)
-            ctx.set_schedule(-1)
+            ctx.set_schedule(args.schedule)
             if p3 != proof:
                 raise SystemExit("serial-schedule proof differs from the overlapped one")
             extra["serial_schedule"] = {"ms_per_step": round(t_ser * 1e3, 3), "steps": ks,
@@ -521,9 +647,12 @@ def main():
         dpk.free()
         if not args.no_msm:
             log("[bench] G1 MSM 2^20 (configs[1])")
-            extra["msm_g1"] = msm_g1_bench(zkp, ctx, 20, args.steps, args.warmup, args.seed + 11)
+            extra["msm_g1"] = msm_g1_bench(zkp, ctx, 20, args.steps, args.warmup, args.seed + 11,
+                                           cpu=not args.no_cpu_baseline)
         if not args.no_cpu_baseline:
-            log(f"[bench] CPU baseline: oracle prove at 2^{log_n_total} on all cores, 2^{args.cpu_log_n} on 1 thread")
+            log(f"[bench] CPU baseline: oracle prove at 2^{log_n_total} on "
+                f"{host_threads_label(oracle_threads())['label']}"
+                f", 2^{args.cpu_log_n} on 1 thread")
             extra["cpu_baseline"] = cpu_baseline(zkp, ctx, n, params, r, s, z_host, proof, args.cpu_log_n,
                                                  args.seed + 21)
             extra["bit_exact_vs_oracle"] = extra["cpu_baseline"]["bit_exact_vs_gpu"]

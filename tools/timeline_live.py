@@ -1,24 +1,22 @@
-"""Unprofiled stream timeline of one prove (tuning): HIP events of the live
-profiler, offsets from the prove's first event (ZK_TIMELINE, common.hpp).
+"""Stream timeline of proves (tuning): HIP events of the live profiler,
+offsets from each prove's first event (zk_ctx_profile(ctx, 2) +
+zk_ctx_timeline_read).
 
   python tools/timeline_live.py [log_n] [schedule]
 """
 import importlib
 import os
 import sys
-import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-path = os.path.join(tempfile.gettempdir(), "zk_timeline.txt")
-os.environ["ZK_TIMELINE"] = path
 import bench  # noqa: E402
 
 
 def main():
     import torch
     log_n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-    sched = int(sys.argv[2]) if len(sys.argv) > 2 else -1
+    sched = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     zkp = importlib.import_module("zero-knowledge-proofs_amd")
     ctx = zkp.Context(0)
     ctx.set_schedule(sched)
@@ -30,14 +28,12 @@ def main():
     for _ in range(3):
         zkp.Prover.prove_device(dpk, z.data_ptr(), 3 * n + 1, 1, r, s)
     torch.cuda.synchronize()
-    if os.path.exists(path):
-        os.remove(path)
-    ctx.profile(True)
+    ctx.profile(2)
     for _ in range(4):
-        pr = zkp.Prover.prove_device(dpk, z.data_ptr(), 3 * n + 1, 1, r, s)
+        zkp.Prover.prove_device(dpk, z.data_ptr(), 3 * n + 1, 1, r, s)
+    text = ctx.timeline_read()
     ctx.profile(False)
-    print("proof b:", pr.serialize_compressed().hex()[96:140], "phases:", sorted(ctx.profile_read().keys()) if False else "")
-    blocks = [b for b in open(path).read().strip().split("--") if b.strip()]
+    blocks = [b for b in text.strip().split("--") if b.strip()]
     for bi, blk in enumerate(blocks[-2:]):
         lines = [ln.split() for ln in blk.strip().splitlines() if ln.strip()]
         streams = {}

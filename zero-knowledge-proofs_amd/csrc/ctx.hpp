@@ -35,7 +35,7 @@ struct zk_ctx {
   zk::MsmWork msm[zk::NUM_MSM];
   std::map<uint32_t, std::unique_ptr<zk::NttDomain>> domains;
   // prove scratch
-  zk::DevBuf z_canon, z_mont, qa, qb, qc, flags;
+  zk::DevBuf z_canon, qabc, flags;   // qabc: the quotient's A, B, C vectors back to back (3n)
   zk::PinnedBuf flags_host;
   zk::DevBuf scal[zk::NUM_MSM];
   zk::DevBuf tmp_scal, tmp_fr;

@@ -370,7 +370,15 @@ constexpr uint32_t ROWCOL_QUAD_MAX = 600;
 //    both decidable from the sorted keys and bucket offsets alone.  A level
 //    reads its children's <= 8 slots in key order, writes buckets that are
 //    now complete and passes the rest up: log4(M/K) levels of <= 7 adds.
-constexpr int MSM_MERGE_FAN = 4;
+// MSM_MERGE_FAN children per group: log_FAN(T) merge launches per MSM,
+// which are no-ops unless some bucket spans more than fix_max chunks
+// (skewed scalars); 8 rather than 4 takes 6 instead of 9 launches off every
+// MSM's tail (each an empty dispatch) at 7 instead of 3 adds per level
+// when they do work.
+#ifndef ZK_MERGE_FAN_LOG
+#define ZK_MERGE_FAN_LOG 3
+#endif
+constexpr int MSM_MERGE_FAN = 1 << ZK_MERGE_FAN_LOG;
 
 // The latency-bound G1 reductions (fixup, row/column sums, quantities, the
 // tree merge) run their adds without the scheduling barriers
@@ -448,7 +456,7 @@ __global__ void __launch_bounds__(128) k_msm_merge(const uint32_t* __restrict__ 
   if (*nbig == 0) return;   // no bucket over fix_max chunks: nothing at any level
   const uint32_t M = off[G];
   const uint32_t K = chunk_len(M, T);
-  const uint64_t W = (uint64_t)K << (2 * level);   // MSM_MERGE_FAN = 4
+  const uint64_t W = (uint64_t)K << (ZK_MERGE_FAN_LOG * level);
   for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;; u += gridDim.x * blockDim.x) {
   const uint64_t s64 = (uint64_t)u * W;
   if (s64 >= M) return;
@@ -727,6 +735,60 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_rowcol_pair(MsmPlan 
   if ((threadIdx.x & 63) < 2) st_pair(&rc[b], v);
 }
 
+// The same sums with W waves per sum (a workgroup each): pair j of the
+// workgroup folds terms j, j + 32 W, ..., a 5-step butterfly combines each
+// wave, and waves 1..W-1 hand their totals to wave 0 through LDS.  The 512
+// sums of a 2^16-bucket MSM otherwise run at half a wave per SIMD (depth
+// 8 + 5 adds); with W = 4: 2 waves per SIMD, depth 2 + 5 + 3.
+#ifndef ZK_RC_PAIR_WAVES
+#define ZK_RC_PAIR_WAVES 4
+#endif
+template <int W>
+__global__ void __launch_bounds__(64 * W) k_msm_rowcol_pair_w(MsmPlan p, const uint32_t* __restrict__ off,
+                                                               const G2X* __restrict__ buckets,
+                                                               G2X* __restrict__ rc) {
+  __shared__ XYZZ<Fq2h> xs[W > 1 ? W - 1 : 1][2];
+  const uint32_t b = blockIdx.x;
+  if (b >= p.nrc) return;   // whole workgroup
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t pr = threadIdx.x >> 1;   // pair index in the workgroup
+  int w = 0;
+  while (b >= p.rcoff[w + 1]) w++;
+  const uint32_t i = b - p.rcoff[w];
+  const uint32_t rows = 1u << p.kr[w], cols = 1u << p.kc[w];
+  uint32_t len, g0, stride;
+  if (i < rows) {
+    len = cols; g0 = p.boff[w] + i * cols; stride = 1;
+  } else {
+    len = rows; g0 = p.boff[w] + (i - rows); stride = cols;
+  }
+  constexpr uint32_t NP = 32 * W;
+  const uint32_t niter = (len + NP - 1) / NP;
+  XYZZ<Fq2h> v;
+  xyzz_set_inf(v);
+#pragma unroll 1
+  for (uint32_t it = 0; it < niter + 5 + (W - 1); it++) {
+    XYZZ<Fq2h> o;
+    if (it < niter) {
+      const uint32_t t = it * NP + pr, g = g0 + t * stride;
+      if (t < len && off[g + 1] != off[g]) o = ld_pair(&buckets[g]);
+      else xyzz_set_inf(o);
+    } else if (it < niter + 5) {
+      o = shfl_xor_point(v, 2 << (it - niter));
+    } else {
+      const uint32_t k = it - niter - 5;
+      if (k == 0) {
+        if (wave && lane < 2) xs[wave - 1][lane] = v;
+        __syncthreads();
+      }
+      if (wave == 0) o = xs[k][lane & 1];
+      else xyzz_set_inf(o);
+    }
+    v = tail_add(v, o);
+  }
+  if (threadIdx.x < 2) st_pair(&rc[b], v);
+}
+
 __global__ void __launch_bounds__(128) k_msm_fixup_pair(const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
                                                         uint32_t fix_max, uint32_t* __restrict__ nbig,
                                                         G2X* __restrict__ buckets, const G2X* __restrict__ partials) {
@@ -864,9 +926,10 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
   {
     X* a = w.partials.as<X>();
     X* b = w.partials2.as<X>();
-    // level l merges groups of 4^l chunks; T chunks at most
-    for (uint32_t level = 1; (1ull << (2 * (level - 1))) < p.T; level++) {
-      const uint32_t groups = (uint32_t)(((uint64_t)p.T + (1ull << (2 * level)) - 1) >> (2 * level));
+    // level l merges groups of FAN^l chunks; T chunks at most
+    for (uint32_t level = 1; (1ull << (ZK_MERGE_FAN_LOG * (level - 1))) < p.T; level++) {
+      const uint32_t groups = (uint32_t)(((uint64_t)p.T + (1ull << (ZK_MERGE_FAN_LOG * level)) - 1) >>
+                                         (ZK_MERGE_FAN_LOG * level));
       // a small grid-stride grid: the common case exits at once and should
       // not queue hundreds of blocks behind other streams' long kernels
       k_msm_merge<C><<<std::min<uint32_t>(ceil_div(groups, 128), 64), 128, 0, st>>>(
@@ -879,9 +942,14 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
   if (pf) pf->end(st, ph);
   ph = pf ? pf->begin(st, (w.tag + "msm_bucket_sum").c_str(), p.G) : -1;   // row/col sums + quantities
   constexpr int RW = ZK_RED_QWAVES;
-  if constexpr (g2)
-    k_msm_rowcol_pair<<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(
-        p, w.off.as<uint32_t>(), reinterpret_cast<const G2X*>(w.buckets.p), reinterpret_cast<G2X*>(w.rc.p));
+  if constexpr (g2) {
+    if constexpr (ZK_RC_PAIR_WAVES > 1)
+      k_msm_rowcol_pair_w<ZK_RC_PAIR_WAVES><<<p.nrc, 64 * ZK_RC_PAIR_WAVES, 0, st>>>(
+          p, w.off.as<uint32_t>(), reinterpret_cast<const G2X*>(w.buckets.p), reinterpret_cast<G2X*>(w.rc.p));
+    else
+      k_msm_rowcol_pair<<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(
+          p, w.off.as<uint32_t>(), reinterpret_cast<const G2X*>(w.buckets.p), reinterpret_cast<G2X*>(w.rc.p));
+  }
   else if (p.nrc <= ROWCOL_QUAD_MAX)
     k_msm_rowcol_q<C, RW><<<p.nrc, 64 * RW, 0, st>>>(p, w.off.as<uint32_t>(), w.buckets.as<X>(), w.rc.as<X>());
   else

@@ -128,6 +128,7 @@ struct PassIO {
   Fr scale;
   uint32_t flags;
   uint32_t* chk = nullptr;   // first pass of an API transform: *chk |= 1 on a non-canonical input
+  uint64_t bstride = 0;      // batch: transform k of the launch works on src / dst + k bstride
 };
 
 // One pass = one four-step level.  The block of N = 2^(s_lo+ns) elements
@@ -152,7 +153,12 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(PassIO io, NttTabs tab
   // blocks (which share 128-byte lines when tiles are 1-2 columns wide) meet
   // in one XCD's L2
   const uint32_t G = gridDim.x;
+  const uint32_t ntiles = (uint32_t)((1ull << log_n) >> (ns + logC));   // per transform
   uint32_t tile = (G & 7) ? blockIdx.x : (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  const uint32_t bi = tile / ntiles;   // transform of a batched launch
+  tile -= bi * ntiles;
+  const Fr* __restrict__ src = io.src + bi * io.bstride;
+  Fr* __restrict__ dst = io.dst + bi * io.bstride;
   const bool gather = io.flags & IO_GATHER;
   if (gather && log_n > ns) tile = bitrev32(tile, log_n - ns);   // gathers of neighbouring tiles share lines
   const uint32_t hi = tile / lo_blocks;
@@ -164,7 +170,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(PassIO io, NttTabs tab
     const uint32_t r = k >> logC, c = k & (C - 1);
     const size_t gi = base + ((size_t)r << s_lo) + c;
     const size_t si = gather ? bitrev32((uint32_t)gi, log_n) : gi;
-    Fr v = ld_vec(&io.src[si]);
+    Fr v = ld_vec(&src[si]);
     if (io.chk && !fr_lt_r(v)) atomicOr(io.chk, 1u);
     if (io.ltab) v = fp_mul(v, ld_vec(&io.ltab[si]));
     if (DIT && s_lo) v = fp_mul(v, tw_full(tabs, ((lo0 + c) * bitrev32(r, ns)) << tw_shift, log_n));
@@ -179,14 +185,14 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(PassIO io, NttTabs tab
     if (!DIT && s_lo) v = fp_mul(v, tw_full(tabs, ((lo0 + c) * bitrev32(r, ns)) << tw_shift, log_n));
     if (io.stab) v = fp_mul(v, ld_vec(&io.stab[go]));
     else if (io.flags & IO_SCALE) v = fp_mul(v, io.scale);
-    st_vec(&io.dst[go], v);
+    st_vec(&dst[go], v);
   }
 }
 
 static void run_pass_io(bool dit, const PassIO& io, const NttTabs& t, uint32_t log_n, uint32_t s_lo, uint32_t ns,
-                        hipStream_t st) {
+                        hipStream_t st, uint32_t nb = 1) {
   const uint32_t logC = std::min<uint32_t>(s_lo, NTT_TILE_LOG - ns);
-  const uint32_t tiles = (uint32_t)((1ull << log_n) >> (ns + logC));
+  const uint32_t tiles = (uint32_t)((1ull << log_n) >> (ns + logC)) * nb;
   const size_t lds = sizeof(Fr) << (ns + logC);
   if (dit)
     k_ntt_pass<true><<<tiles, NTT_THREADS, lds, st>>>(io, t, log_n, s_lo, ns, logC);
@@ -196,8 +202,10 @@ static void run_pass_io(bool dit, const PassIO& io, const NttTabs& t, uint32_t l
 }
 
 static void run_pass(bool dit, Fr* d, const NttTabs& t, uint32_t log_n, uint32_t s_lo, uint32_t ns,
-                     hipStream_t st, const Fr* src = nullptr, const Fr* ltab = nullptr) {
-  run_pass_io(dit, PassIO{src ? src : d, d, ltab, nullptr, Fr{}, 0u}, t, log_n, s_lo, ns, st);
+                     hipStream_t st, const Fr* src = nullptr, const Fr* ltab = nullptr, uint32_t nb = 1) {
+  PassIO io{src ? src : d, d, ltab, nullptr, Fr{}, 0u};
+  io.bstride = (uint64_t)1 << log_n;
+  run_pass_io(dit, io, t, log_n, s_lo, ns, st, nb);
 }
 
 // Pass plan, top (first DIF pass) to bottom: the contiguous pass (s_lo = 0)
@@ -220,30 +228,31 @@ static std::vector<uint32_t> pass_plan(uint32_t L) {
 }
 
 
-void ntt_dif(Fr* d, const NttDomain& dom, bool inv, hipStream_t st, Prof* pf, const Fr* src, const Fr* ltab) {
+void ntt_dif(Fr* d, const NttDomain& dom, bool inv, hipStream_t st, Prof* pf, const Fr* src, const Fr* ltab,
+             uint32_t nb) {
   const uint32_t L = dom.log_n;
   if (L == 0) return;
-  const int ph = pf ? pf->begin(st, "ntt", (uint64_t)1 << L) : -1;
+  const int ph = pf ? pf->begin(st, "ntt", (uint64_t)nb << L) : -1;
   const NttTabs t = tabs_of(dom, inv);
   uint32_t s_hi = L;
   bool first = true;
   for (uint32_t ns : pass_plan(L)) {
-    run_pass(false, d, t, L, s_hi - ns, ns, st, first ? src : nullptr, first ? ltab : nullptr);
+    run_pass(false, d, t, L, s_hi - ns, ns, st, first ? src : nullptr, first ? ltab : nullptr, nb);
     first = false;
     s_hi -= ns;
   }
   if (pf) pf->end(st, ph);
 }
 
-void ntt_dit(Fr* d, const NttDomain& dom, bool inv, hipStream_t st, Prof* pf) {
+void ntt_dit(Fr* d, const NttDomain& dom, bool inv, hipStream_t st, Prof* pf, uint32_t nb) {
   const uint32_t L = dom.log_n;
   if (L == 0) return;
-  const int ph = pf ? pf->begin(st, "ntt", (uint64_t)1 << L) : -1;
+  const int ph = pf ? pf->begin(st, "ntt", (uint64_t)nb << L) : -1;
   const NttTabs t = tabs_of(dom, inv);
   const std::vector<uint32_t> plan = pass_plan(L);
   uint32_t s_lo = 0;
   for (auto it = plan.rbegin(); it != plan.rend(); ++it) {
-    run_pass(true, d, t, L, s_lo, *it, st);
+    run_pass(true, d, t, L, s_lo, *it, st, nullptr, nullptr, nb);
     s_lo += *it;
   }
   if (pf) pf->end(st, ph);
@@ -293,46 +302,51 @@ void ntt_natural(Fr* dst, const Fr* src, Fr* tmp, const NttDomain& dom, bool inv
 // new 128-B line and, beyond the MALL, a new page per element) and runs
 // the DIT stages with the forward twiddles while the tile stays in LDS: two
 // HBM round trips and the separate scale pass disappear.
+// Batched: the launch covers nb transforms of 2^log_n elements back to back
+// in data (block b works on tile b mod tiles of transform b / tiles).
 __global__ void __launch_bounds__(NTT_THREADS) k_ntt_tile_shift(Fr* __restrict__ data, const Fr* __restrict__ ism,
                                                                const Fr* __restrict__ sm,
-                                                               const Fr* __restrict__ tab_br, uint32_t ns) {
+                                                               const Fr* __restrict__ tab_br, uint32_t ns,
+                                                               uint32_t log_n) {
   extern __shared__ uint4 sh_raw[];
   Fr* sh = reinterpret_cast<Fr*>(sh_raw);
   const uint32_t tile_elems = 1u << ns;
   const size_t base = (size_t)blockIdx.x << ns;
+  const size_t tbase = base & (((size_t)1 << log_n) - 1);   // position within its transform
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) st_vec(&sh[k], ld_vec(&data[base + k]));
   __syncthreads();
   ntt_rounds<false>(sh, ism, ns, 0);
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) {
-    st_vec(&sh[k], fp_mul(ld_vec(&sh[k]), ld_vec(&tab_br[base + k])));
+    st_vec(&sh[k], fp_mul(ld_vec(&sh[k]), ld_vec(&tab_br[tbase + k])));
   }
   __syncthreads();
   ntt_rounds<true>(sh, sm, ns, 0);
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) st_vec(&data[base + k], ld_vec(&sh[k]));
 }
 
-void ntt_coset_shift(Fr* d, const NttDomain& dom, const Fr* tab_br, hipStream_t st, Prof* pf) {
+void ntt_coset_shift(Fr* d, const NttDomain& dom, const Fr* tab_br, hipStream_t st, Prof* pf, uint32_t nb) {
   const uint32_t L = dom.log_n;
   if (L == 0) {
-    fr_scale_table(d, tab_br, 0, false, st);
+    fr_scale_table(d, tab_br, 0, false, st, nb);
     return;
   }
-  const int ph = pf ? pf->begin(st, "ntt", (uint64_t)2 << L) : -1;
+  const int ph = pf ? pf->begin(st, "ntt", (uint64_t)(2 * nb) << L) : -1;
   const NttTabs ti = tabs_of(dom, true), tf = tabs_of(dom, false);
   const std::vector<uint32_t> plan = pass_plan(L);
   // inverse transform: every DIF pass but the last (contiguous) one
   uint32_t s_hi = L;
   for (size_t i = 0; i + 1 < plan.size(); i++) {
-    run_pass(false, d, ti, L, s_hi - plan[i], plan[i], st);
+    run_pass(false, d, ti, L, s_hi - plan[i], plan[i], st, nullptr, nullptr, nb);
     s_hi -= plan[i];
   }
   const uint32_t ns = plan.back();   // s_hi == ns here: the contiguous pass
-  k_ntt_tile_shift<<<(uint32_t)((1ull << L) >> ns), NTT_THREADS, sizeof(Fr) << ns, st>>>(d, ti.sm, tf.sm, tab_br, ns);
+  k_ntt_tile_shift<<<(uint32_t)(((uint64_t)nb << L) >> ns), NTT_THREADS, sizeof(Fr) << ns, st>>>(d, ti.sm, tf.sm,
+                                                                                                tab_br, ns, L);
   ZK_LAUNCH_CHECK();
   // forward transform: every DIT pass but the first (contiguous) one
   uint32_t s_lo = ns;
   for (size_t i = plan.size() - 1; i-- > 0;) {
-    run_pass(true, d, tf, L, s_lo, plan[i], st);
+    run_pass(true, d, tf, L, s_lo, plan[i], st, nullptr, nullptr, nb);
     s_lo += plan[i];
   }
   if (pf) pf->end(st, ph);
@@ -470,11 +484,12 @@ __global__ void __launch_bounds__(256) k_from_mont(const Fr* __restrict__ in, ui
   st_vec(reinterpret_cast<Fr*>(out) + i, fp_from_mont(ld_vec(&in[i])));
 }
 __global__ void __launch_bounds__(256) k_scale_table(Fr* __restrict__ d, const Fr* __restrict__ tab,
-                                                     uint32_t log_n, bool bitrev) {
-  const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >> log_n) return;
+                                                     uint32_t log_n, bool bitrev, uint32_t nb) {
+  const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((q >> log_n) >= nb) return;
+  const size_t p = q & (((size_t)1 << log_n) - 1);   // batched: the same table for every transform
   const size_t j = bitrev ? bitrev32((uint32_t)p, log_n) : p;
-  st_vec(&d[p], fp_mul(ld_vec(&d[p]), ld_vec(&tab[j])));
+  st_vec(&d[q], fp_mul(ld_vec(&d[q]), ld_vec(&tab[j])));
 }
 __global__ void __launch_bounds__(256) k_bitrev_copy(const Fr* __restrict__ in, Fr* __restrict__ out, uint32_t log_n) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -544,8 +559,8 @@ void fr_from_mont(const Fr* d_in, uint64_t* d_canon, size_t n, hipStream_t st) {
   k_from_mont<<<ceil_div(n, 256), 256, 0, st>>>(d_in, d_canon, n);
   ZK_LAUNCH_CHECK();
 }
-void fr_scale_table(Fr* d, const Fr* tab, uint32_t log_n, bool bitrev, hipStream_t st) {
-  k_scale_table<<<ceil_div((size_t)1 << log_n, 256), 256, 0, st>>>(d, tab, log_n, bitrev);
+void fr_scale_table(Fr* d, const Fr* tab, uint32_t log_n, bool bitrev, hipStream_t st, uint32_t nb) {
+  k_scale_table<<<ceil_div((size_t)nb << log_n, 256), 256, 0, st>>>(d, tab, log_n, bitrev, nb);
   ZK_LAUNCH_CHECK();
 }
 void fr_bitrev_copy(const Fr* in, Fr* out, uint32_t log_n, hipStream_t st) {

@@ -76,12 +76,14 @@ inline NttTabs tabs_of(const NttDomain& dom, bool inv) {
 }
 
 
-// In-place passes over n Montgomery Fr.
+// In-place passes over n Montgomery Fr; nb > 1: nb transforms back to back
+// in d_data (n apart), every pass one launch for all of them.
 // ntt_dif's first pass may read `src` instead of d_data (out of place) and
 // multiply each loaded element by ltab[i] (natural index), e.g. a coset's g^i.
 void ntt_dif(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st, Prof* pf = nullptr,
-             const Fr* src = nullptr, const Fr* ltab = nullptr);
-void ntt_dit(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st, Prof* pf = nullptr);
+             const Fr* src = nullptr, const Fr* ltab = nullptr, uint32_t nb = 1);
+void ntt_dit(Fr* d_data, const NttDomain& dom, bool inverse_twiddles, hipStream_t st, Prof* pf = nullptr,
+             uint32_t nb = 1);
 // Natural order in (src) and out (dst), the API transform: DIT passes whose
 // first pass gathers from bit-reversed positions; ltab: factor on the input
 // (natural index), stab / scale: factor on the output.  tmp: n elements of
@@ -95,12 +97,14 @@ void ntt_natural(Fr* dst, const Fr* src, Fr* tmp, const NttDomain& dom, bool inv
 // quotient's coefficients -> coset evaluations step).  tab_br is the factor
 // table in bit-reversed order (NttDomain::gpow_br: n^-1 g^bitrev(p)), so the
 // tile reads it contiguously instead of gathering 32-B words across n.
-void ntt_coset_shift(Fr* d_data, const NttDomain& dom, const Fr* d_tab_br, hipStream_t st, Prof* pf = nullptr);
+void ntt_coset_shift(Fr* d_data, const NttDomain& dom, const Fr* d_tab_br, hipStream_t st, Prof* pf = nullptr,
+                     uint32_t nb = 1);
 // Elementwise helpers
 void fr_to_mont(const uint64_t* d_canon, Fr* d_out, size_t n, hipStream_t st);
 void fr_from_mont(const Fr* d_in, uint64_t* d_canon, size_t n, hipStream_t st);
-// data[p] *= tab[bitrev(p)] (bitrev over log_n bits)  or  tab[p] when !bitrev
-void fr_scale_table(Fr* d_data, const Fr* d_tab, uint32_t log_n, bool bitrev, hipStream_t st);
+// data[p] *= tab[bitrev(p)] (bitrev over log_n bits)  or  tab[p] when !bitrev;
+// nb transforms of 2^log_n back to back, the same table for each
+void fr_scale_table(Fr* d_data, const Fr* d_tab, uint32_t log_n, bool bitrev, hipStream_t st, uint32_t nb = 1);
 // out[i] = in[bitrev(i)] (out-of-place)
 void fr_bitrev_copy(const Fr* d_in, Fr* d_out, uint32_t log_n, hipStream_t st);
 // out[bitrev(i)] = in[i] * f, f = tab[bitrev(i)] (tab != nullptr), else c

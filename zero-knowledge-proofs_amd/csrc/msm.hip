@@ -372,11 +372,10 @@ constexpr uint32_t ROWCOL_QUAD_MAX = 600;
 //    now complete and passes the rest up: log4(M/K) levels of <= 7 adds.
 // MSM_MERGE_FAN children per group: log_FAN(T) merge launches per MSM,
 // which are no-ops unless some bucket spans more than fix_max chunks
-// (skewed scalars); 8 rather than 4 takes 6 instead of 9 launches off every
-// MSM's tail (each an empty dispatch) at 7 instead of 3 adds per level
-// when they do work.
+// (skewed scalars).  Fan-out 8 (6 instead of 9 launches) measured 0.36 ms
+// SLOWER in the overlapped prove (profiles/r03_ab_batchq_fan8_rcw4_rejected.txt).
 #ifndef ZK_MERGE_FAN_LOG
-#define ZK_MERGE_FAN_LOG 3
+#define ZK_MERGE_FAN_LOG 2
 #endif
 constexpr int MSM_MERGE_FAN = 1 << ZK_MERGE_FAN_LOG;
 
@@ -735,60 +734,6 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_rowcol_pair(MsmPlan 
   if ((threadIdx.x & 63) < 2) st_pair(&rc[b], v);
 }
 
-// The same sums with W waves per sum (a workgroup each): pair j of the
-// workgroup folds terms j, j + 32 W, ..., a 5-step butterfly combines each
-// wave, and waves 1..W-1 hand their totals to wave 0 through LDS.  The 512
-// sums of a 2^16-bucket MSM otherwise run at half a wave per SIMD (depth
-// 8 + 5 adds); with W = 4: 2 waves per SIMD, depth 2 + 5 + 3.
-#ifndef ZK_RC_PAIR_WAVES
-#define ZK_RC_PAIR_WAVES 4
-#endif
-template <int W>
-__global__ void __launch_bounds__(64 * W) k_msm_rowcol_pair_w(MsmPlan p, const uint32_t* __restrict__ off,
-                                                               const G2X* __restrict__ buckets,
-                                                               G2X* __restrict__ rc) {
-  __shared__ XYZZ<Fq2h> xs[W > 1 ? W - 1 : 1][2];
-  const uint32_t b = blockIdx.x;
-  if (b >= p.nrc) return;   // whole workgroup
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t pr = threadIdx.x >> 1;   // pair index in the workgroup
-  int w = 0;
-  while (b >= p.rcoff[w + 1]) w++;
-  const uint32_t i = b - p.rcoff[w];
-  const uint32_t rows = 1u << p.kr[w], cols = 1u << p.kc[w];
-  uint32_t len, g0, stride;
-  if (i < rows) {
-    len = cols; g0 = p.boff[w] + i * cols; stride = 1;
-  } else {
-    len = rows; g0 = p.boff[w] + (i - rows); stride = cols;
-  }
-  constexpr uint32_t NP = 32 * W;
-  const uint32_t niter = (len + NP - 1) / NP;
-  XYZZ<Fq2h> v;
-  xyzz_set_inf(v);
-#pragma unroll 1
-  for (uint32_t it = 0; it < niter + 5 + (W - 1); it++) {
-    XYZZ<Fq2h> o;
-    if (it < niter) {
-      const uint32_t t = it * NP + pr, g = g0 + t * stride;
-      if (t < len && off[g + 1] != off[g]) o = ld_pair(&buckets[g]);
-      else xyzz_set_inf(o);
-    } else if (it < niter + 5) {
-      o = shfl_xor_point(v, 2 << (it - niter));
-    } else {
-      const uint32_t k = it - niter - 5;
-      if (k == 0) {
-        if (wave && lane < 2) xs[wave - 1][lane] = v;
-        __syncthreads();
-      }
-      if (wave == 0) o = xs[k][lane & 1];
-      else xyzz_set_inf(o);
-    }
-    v = tail_add(v, o);
-  }
-  if (threadIdx.x < 2) st_pair(&rc[b], v);
-}
-
 __global__ void __launch_bounds__(128) k_msm_fixup_pair(const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
                                                         uint32_t fix_max, uint32_t* __restrict__ nbig,
                                                         G2X* __restrict__ buckets, const G2X* __restrict__ partials) {
@@ -942,14 +887,9 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
   if (pf) pf->end(st, ph);
   ph = pf ? pf->begin(st, (w.tag + "msm_bucket_sum").c_str(), p.G) : -1;   // row/col sums + quantities
   constexpr int RW = ZK_RED_QWAVES;
-  if constexpr (g2) {
-    if constexpr (ZK_RC_PAIR_WAVES > 1)
-      k_msm_rowcol_pair_w<ZK_RC_PAIR_WAVES><<<p.nrc, 64 * ZK_RC_PAIR_WAVES, 0, st>>>(
-          p, w.off.as<uint32_t>(), reinterpret_cast<const G2X*>(w.buckets.p), reinterpret_cast<G2X*>(w.rc.p));
-    else
-      k_msm_rowcol_pair<<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(
-          p, w.off.as<uint32_t>(), reinterpret_cast<const G2X*>(w.buckets.p), reinterpret_cast<G2X*>(w.rc.p));
-  }
+  if constexpr (g2)
+    k_msm_rowcol_pair<<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(
+        p, w.off.as<uint32_t>(), reinterpret_cast<const G2X*>(w.buckets.p), reinterpret_cast<G2X*>(w.rc.p));
   else if (p.nrc <= ROWCOL_QUAD_MAX)
     k_msm_rowcol_q<C, RW><<<p.nrc, 64 * RW, 0, st>>>(p, w.off.as<uint32_t>(), w.buckets.as<X>(), w.rc.as<X>());
   else

@@ -426,25 +426,27 @@ static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipS
   ZK_LAUNCH_CHECK();
   pf->end(st, ph);
   // per polynomial: iNTT (coefficients * n, bit-reversed), * n^-1 g^i, NTT
-  // (evaluations on the coset g<w>, natural order), the three polynomials
-  // batched into every launch (3x the workgroups: fewer launches and round
-  // tails).  Fused into one tile kernel below 2^LARGE_Q_LOG; from there the
-  // three steps run as separate passes, and the final coset iNTT runs in
-  // natural order (ntt_natural) instead of a DIF plus an element-wise
-  // bit-reversed gather.  Same-box A/B, overlapped prove: 2^24 fused 122.8 /
-  // separate 118.6 ms; 2^20 the gather path 9.89 / natural 10.01 ms
-  // (profiles/r02_ab_quot.txt).
+  // (evaluations on the coset g<w>, natural order).  Fused into one tile
+  // kernel below 2^LARGE_Q_LOG; from there the three steps run as separate
+  // passes, and the final coset iNTT runs in natural order (ntt_natural)
+  // instead of a DIF plus an element-wise bit-reversed gather.  Same-box
+  // A/B, overlapped prove: 2^24 fused 122.8 / separate 118.6 ms; 2^20 the
+  // gather path 9.89 / natural 10.01 ms (profiles/r02_ab_quot.txt).  One
+  // launch per pass for all three polynomials (nb = 3) lost 0.2 ms in the
+  // overlapped prove (profiles/r03_ab_batchq_fan8_rcw4_rejected.txt).
   // zk_ctx_set_option(ZK_OPT_QUOTIENT_PATH) forces either path (tests).
   constexpr uint32_t LARGE_Q_LOG = 23;
   const bool large = ctx->quot_path >= 0 ? ctx->quot_path == 1 : pk->log_n >= LARGE_Q_LOG;
-  if (!large) {
-    ntt_coset_shift(v[0], dom, domain_gpow_br(dom, st), st, pf, 3);
-  } else {
-    ntt_dif(v[0], dom, /*inverse twiddles*/ true, st, pf, nullptr, nullptr, 3);
-    ph = pf->begin(st, "quotient_misc", 3 * n);
-    fr_scale_table(v[0], domain_gpow_br(dom, st), pk->log_n, false, st, 3);
+  for (int k = 0; k < 3; k++) {
+    if (!large) {
+      ntt_coset_shift(v[k], dom, domain_gpow_br(dom, st), st, pf);
+      continue;
+    }
+    ntt_dif(v[k], dom, /*inverse twiddles*/ true, st, pf);
+    ph = pf->begin(st, "quotient_misc", n);
+    fr_scale_table(v[k], domain_gpow_br(dom, st), pk->log_n, false, st);
     pf->end(st, ph);
-    ntt_dit(v[0], dom, false, st, pf, 3);
+    ntt_dit(v[k], dom, false, st, pf);
   }
   ph = pf->begin(st, "quotient_misc", n);
   k_quot_pointwise<<<ceil_div(n, 256), 256, 0, st>>>(v[0], v[1], v[2], dom.zinv.as<Fr>(), n);

@@ -6,7 +6,12 @@
 
 namespace zk {
 
-constexpr int NTT_TILE_LOG = 11;  // 2048 elements x 32 B = 64 KiB of LDS per workgroup
+// 2^NTT_TILE_LOG elements per tile: 2048 x 32 B = 64 KiB of LDS per workgroup
+// (ZK_NTT_TILE_LOG: A/B builds only)
+#ifndef ZK_NTT_TILE_LOG
+#define ZK_NTT_TILE_LOG 11
+#endif
+constexpr int NTT_TILE_LOG = ZK_NTT_TILE_LOG;
 // Radix of the register rounds (2^NTT_R elements per thread) and threads per
 // tile: one group per thread for a full tile.
 #ifndef ZK_NTT_R

@@ -571,21 +571,24 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
     ZK_HIP(hipEventRecord(ctx->ev_done[slots[0]], gs));
   };
   // G2 (pi_B), then A + B1 + IC, both starting with the witness
-  if (!serial) ZK_HIP(hipStreamWaitEvent(s_g2, ctx->ev_scal, 0));
-  {
-    Range range("msm_g2");
-    MsmWork& w = ctx->msm[MSM_B2];
-    w.tag = serial ? tags[MSM_B2] : "";
-    prep_scalars(MSM_B2, s_g2);
-    msm_launch_shared<G2>(w, pk->bases[MSM_B2].as<G2A>(), ctx->scal[MSM_B2].as<uint64_t>(), 1,
-                          pk->count[MSM_B2] + pk->extras[MSM_B2], 64, pk->win_c, s_g2, pk->stride[MSM_B2]);
-    msm_download<G2>(w, s_g2);
-    ZK_HIP(hipEventRecord(ctx->ev_done[MSM_B2], s_g2));
-  }
-  if (!serial) ZK_HIP(hipStreamWaitEvent(s_abi, ctx->ev_scal, 0));
-  launch_batch(G1_ABI, 3, "ABI/", s_abi);
+  auto launch_msms = [&]() {
+    if (!serial) ZK_HIP(hipStreamWaitEvent(s_g2, ctx->ev_scal, 0));
+    {
+      Range range("msm_g2");
+      MsmWork& w = ctx->msm[MSM_B2];
+      w.tag = serial ? tags[MSM_B2] : "";
+      prep_scalars(MSM_B2, s_g2);
+      msm_launch_shared<G2>(w, pk->bases[MSM_B2].as<G2A>(), ctx->scal[MSM_B2].as<uint64_t>(), 1,
+                            pk->count[MSM_B2] + pk->extras[MSM_B2], 64, pk->win_c, s_g2, pk->stride[MSM_B2]);
+      msm_download<G2>(w, s_g2);
+      ZK_HIP(hipEventRecord(ctx->ev_done[MSM_B2], s_g2));
+    }
+    if (!serial) ZK_HIP(hipStreamWaitEvent(s_abi, ctx->ev_scal, 0));
+    launch_batch(G1_ABI, 3, "ABI/", s_abi);
+  };
   // the quotient, then H on the main stream
-  if (!h_given) {
+  auto run_quotient = [&]() {
+    if (h_given) return;
     Range range(dist ? "quotient_distributed" : "quotient");
     if (dist) {
       ctx->tmp_scal.ensure(sizeof(uint64_t) * (pk->n / pk->nshards));
@@ -595,6 +598,18 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       quotient(ctx, pk, d_z, st);   // (Az, Bz, Cz) -> lo64(H) in tmp_scal
       h_src = ctx->tmp_scal.as<uint64_t>();
     }
+  };
+  // The quotient heads the chain that ends the proof (quotient -> H sort ->
+  // H accumulate -> H tail), so its kernels are enqueued first: the GPU
+  // sees them before the G2 accumulate's full-occupancy round.  A host-staged
+  // exchange blocks this thread inside the quotient, so then the MSMs go
+  // first.
+  if (dist && ctx->exch->host_blocking()) {
+    launch_msms();
+    run_quotient();
+  } else {
+    run_quotient();
+    launch_msms();
   }
   ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
   {

@@ -375,7 +375,6 @@ struct HostExchange : Exchange {
   void abort() override {
     if (ops.abort) ops.abort(ops.user);
   }
-  bool host_blocking() const override { return true; }
 };
 
 std::unique_ptr<Exchange> make_host_exchange(const zk_exchange_ops& ops, int rank, int world) {

@@ -41,8 +41,6 @@ struct Exchange {
   virtual void abort() = 0;
   // an asynchronous transport error is pending (RCCL: ncclCommGetAsyncError)
   virtual bool async_error() { return false; }
-  // all_to_all runs on (and blocks) the calling host thread
-  virtual bool host_blocking() const { return false; }
   // watchdog for waits on work that depends on the peers: give up (throw
   // ZK_ERR_RCCL) after this long or on an asynchronous transport error
   double timeout_ms = 60000;

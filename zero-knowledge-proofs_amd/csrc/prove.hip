@@ -599,18 +599,10 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       h_src = ctx->tmp_scal.as<uint64_t>();
     }
   };
-  // The quotient heads the chain that ends the proof (quotient -> H sort ->
-  // H accumulate -> H tail), so its kernels are enqueued first: the GPU
-  // sees them before the G2 accumulate's full-occupancy round.  A host-staged
-  // exchange blocks this thread inside the quotient, so then the MSMs go
-  // first.
-  if (dist && ctx->exch->host_blocking()) {
-    launch_msms();
-    run_quotient();
-  } else {
-    run_quotient();
-    launch_msms();
-  }
+  // MSMs first, then the quotient (enqueueing the quotient first measured
+  // 0.37 ms slower: profiles/r03_ab_quotient_first_rejected.txt)
+  launch_msms();
+  run_quotient();
   ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
   {
     const int h_slot[1] = {MSM_H};

@@ -239,6 +239,21 @@ struct EntQ {
 #else
 #define ZK_ACCUM_ATTR
 #endif
+// A/B builds: register caps on the accumulates (ZK_ACCUM_G1_WPE /
+// ZK_ACCUM_G2_WPE waves per SIMD worth of registers) with the launch sized
+// for ZK_ACCUM_G1_WAVES / ZK_ACCUM_G2_WAVES waves per SIMD, so that a full
+// accumulate round leaves registers for other streams' kernels (quotient,
+// sorts) on every SIMD
+#ifdef ZK_ACCUM_G1_WPE
+#define ZK_ACCUM_G1_ATTR __attribute__((amdgpu_waves_per_eu(ZK_ACCUM_G1_WPE)))
+#else
+#define ZK_ACCUM_G1_ATTR ZK_ACCUM_ATTR
+#endif
+#ifdef ZK_ACCUM_G2_WPE
+#define ZK_ACCUM_G2_ATTR __attribute__((amdgpu_waves_per_eu(ZK_ACCUM_G2_WPE)))
+#else
+#define ZK_ACCUM_G2_ATTR ZK_ACCUM_ATTR
+#endif
 template <class A>
 struct SegBases {
   const char* p[MSM_MAXSEG];
@@ -255,7 +270,7 @@ ZK_DI const A* seg_base(const SegBases<A>& sb, uint32_t seg, uint32_t i) {
 }
 
 template <class C>
-__global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum(SegBases<typename C::A> sb, uint32_t segshift,
+__global__ void __launch_bounds__(128) ZK_ACCUM_G1_ATTR k_msm_accum(SegBases<typename C::A> sb, uint32_t segshift,
                                                    const uint32_t* __restrict__ ent,
                                                    const uint32_t* __restrict__ key,
                                                    const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
@@ -308,7 +323,7 @@ ZK_DI void st_pair(G2X* p, const XYZZ<Fq2h>& a) {
   st_vec(q + 4, a.ZZ.v);
   st_vec(q + 6, a.ZZZ.v);
 }
-__global__ void __launch_bounds__(128) ZK_ACCUM_ATTR k_msm_accum_pair(SegBases<G2A> sb, uint32_t segshift,
+__global__ void __launch_bounds__(128) ZK_ACCUM_G2_ATTR k_msm_accum_pair(SegBases<G2A> sb, uint32_t segshift,
                                                                       const uint32_t* __restrict__ ent,
                                                                       const uint32_t* __restrict__ key,
                                                                       const uint32_t* __restrict__ off, uint32_t G,
@@ -771,6 +786,12 @@ static uint32_t accum_threads() {
       ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_accum_pair, 128, 0));
     else
       ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_accum<C>, 128, 0));
+#ifdef ZK_ACCUM_G1_WAVES
+    if constexpr (!pair) per_cu = std::min(per_cu, ZK_ACCUM_G1_WAVES * 2);   // 128-thread blocks: 2 waves
+#endif
+#ifdef ZK_ACCUM_G2_WAVES
+    if constexpr (pair) per_cu = std::min(per_cu, ZK_ACCUM_G2_WAVES * 2);
+#endif
     return (uint32_t)std::max(1, per_cu * cus * (pair ? 64 : 128));
   }();
   return T;

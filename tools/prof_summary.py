@@ -169,7 +169,7 @@ def pmc_prove(fetch_db, write_db, out, factor):
                    "traffic_guide_2x": int((2 * fb + wb) / n), "traffic_calibrated": int((factor * fb + wb) / n)}
                for k, (n, fb, wb) in sorted(agg.items())}
     acc = [(fv * 1024, wv * 1024) for (_, k, fv), (_, _, wv) in zip(fd, wd) if "k_msm_accum" in k and "pair" not in k]
-    res = {"note": f"serial prove (ZK_PROVE_SCHED=3); traffic_calibrated = {factor} x FETCH_SIZE + WRITE_SIZE "
+    res = {"note": f"serial prove (zk_ctx_set_schedule 3); traffic_calibrated = {factor} x FETCH_SIZE + WRITE_SIZE "
                    "(FETCH factor from tools/gather_calib for the accumulate's gather shape -- 1.779 for 96-byte "
                    "points read at a 128-byte stride (k_gather<6,8>), 1.585 for packed 96-byte points -- "
                    "profiles/r02_fetch_calibration.json); traffic_guide_2x = the guide's streaming correction",
@@ -188,7 +188,47 @@ def pmc_prove(fetch_db, write_db, out, factor):
             print(k, v)
 
 
+def part(fetch_db, write_db, out, kind, calls, factor):
+    """HBM traffic of one standalone workload (tools/msm_only.py or
+    tools/ntt_only.py ... fwd) from its FETCH_SIZE and WRITE_SIZE passes.
+    msm: bytes per k_msm_accum<G1> launch (FETCH x `factor`, the gather
+    calibration); ntt: bytes per forward transform = every dispatch of the
+    run / `calls` (FETCH x 2, the guide's streaming correction)."""
+    fd, wd = dispatches(fetch_db, "FETCH_SIZE"), dispatches(write_db, "WRITE_SIZE")
+    assert len(fd) == len(wd), (len(fd), len(wd))
+    agg = {}
+    for (_, k, fv), (_, k2, wv) in zip(fd, wd):
+        assert k == k2
+        a = agg.setdefault(short(k), [0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += fv * 1024
+        a[2] += wv * 1024
+    f = factor if kind == "msm" else 2.0
+    kernels = {k: {"dispatches": n, "fetch_bytes": int(fb / n), "write_bytes": int(wb / n),
+                   "traffic_bytes": int((f * fb + wb) / n)} for k, (n, fb, wb) in sorted(agg.items())}
+    res = {"kind": kind, "calls": calls, "fetch_factor": f, "kernels": kernels}
+    if kind == "msm":
+        acc = [(fv * 1024, wv * 1024) for (_, k, fv), (_, _, wv) in zip(fd, wd)
+               if "k_msm_accum" in k and "pair" not in k]
+        res["bytes_per_launch"] = int(sum(f * a + b for a, b in acc) / len(acc))
+        per_call = [(fv * 1024, wv * 1024) for (_, k, fv), (_, _, wv) in zip(fd, wd)
+                    if "k_msm" in k or "rocprim" in k]   # not the setup / base upload kernels
+        res["whole_msm_bytes_per_call"] = int(sum(f * a + b for a, b in per_call) / calls)
+        res["note"] = ("tools/msm_only.py: 2^20 bases x 13 window copies (c = 20), 255-bit scalars; "
+                       f"bytes_per_launch = {f} x FETCH_SIZE + WRITE_SIZE of k_msm_accum<G1> "
+                       "(FETCH factor from tools/gather_calib, profiles/r02_fetch_calibration.json)")
+    else:
+        res["bytes_per_launch"] = int(sum(f * v[1] + v[2] for v in agg.values()) / calls)
+        res["note"] = ("tools/ntt_only.py ... fwd: forward zk_ntt_fr_dev calls only; bytes_per_launch = "
+                       "2 x FETCH_SIZE + WRITE_SIZE over every dispatch / calls, i.e. per transform")
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
+
+
 if __name__ == "__main__":
+    if sys.argv[1] == "part":
+        part(sys.argv[2], sys.argv[3], sys.argv[4], sys.argv[5], int(sys.argv[6]), float(sys.argv[7]))
+        sys.exit(0)
     if sys.argv[1] == "calib":
         calib(sys.argv[2], sys.argv[3], sys.argv[4], sys.argv[5])
         sys.exit(0)

@@ -514,6 +514,45 @@ __global__ void __launch_bounds__(128) k_msm_merge(const uint32_t* __restrict__ 
 
 constexpr int MSM_RED_WAVES = 4;   // sums per 256-thread workgroup
 
+// Partial row/column sum b of the plan: its window, and the buckets it folds
+// (len buckets from g0 at stride).  Row i's partial s covers columns
+// [s len, (s + 1) len), column j's partial s rows [s len, (s + 1) len).
+struct SumSpan {
+  uint32_t len, g0, stride;
+};
+ZK_DI SumSpan rowcol_span(const MsmPlan& p, uint32_t b) {
+  int w = 0;
+  while (b >= p.rcoff[w + 1]) w++;
+  const uint32_t i = b - p.rcoff[w];
+  const uint32_t kr = p.kr[w], kc = p.kc[w], lsr = p.lsr[w], lsc = p.lsc[w];
+  const uint32_t nr = 1u << (kr + lsr);
+  if (i < nr) {
+    const uint32_t len = 1u << (kc - lsr);
+    return {len, p.boff[w] + ((i >> lsr) << kc) + (i & ((1u << lsr) - 1)) * len, 1u};
+  }
+  const uint32_t j = i - nr, len = 1u << (kr - lsc);
+  return {len, p.boff[w] + (j >> lsc) + (((j & ((1u << lsc) - 1)) * len) << kc), 1u << kc};
+}
+
+// Quantity q of the plan: U^C_b (row partials whose row has bit b), U^D_b
+// (column partials whose column has bit b) or P (all column partials).
+struct QuantSpan {
+  uint32_t len, src, bit, shift;   // bit 32: every term
+};
+ZK_DI QuantSpan quant_span(const MsmPlan& p, uint32_t b) {
+  int w = 0;
+  while (b >= p.qoff[w + 1]) w++;
+  const uint32_t q = b - p.qoff[w];
+  const uint32_t kr = p.kr[w], kc = p.kc[w], lsr = p.lsr[w], lsc = p.lsc[w];
+  const uint32_t nr = 1u << (kr + lsr), nc = 1u << (kc + lsc);
+  if (q < kr) return {nr, p.rcoff[w], q, lsr};
+  if (q < kr + kc) return {nc, p.rcoff[w] + nr, q - kr, lsc};
+  return {nc, p.rcoff[w] + nr, 32u, 0u};
+}
+ZK_DI bool quant_has(const QuantSpan& s, uint32_t t) {
+  return t < s.len && (s.bit == 32 || ((t >> (s.bit + s.shift)) & 1));
+}
+
 // Row sums C_hi (2^kc contiguous buckets) and column sums D_lo (2^kr buckets
 // at stride 2^kc) of every window, one wave each.
 template <class C>
@@ -524,16 +563,8 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_rowcol(MsmPlan p, co
   const uint32_t b = blockIdx.x * MSM_RED_WAVES + (threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
   if (b >= p.nrc) return;   // whole waves
-  int w = 0;
-  while (b >= p.rcoff[w + 1]) w++;
-  const uint32_t i = b - p.rcoff[w];
-  const uint32_t rows = 1u << p.kr[w], cols = 1u << p.kc[w];
-  uint32_t len, g0, stride;
-  if (i < rows) {
-    len = cols; g0 = p.boff[w] + i * cols; stride = 1;
-  } else {
-    len = rows; g0 = p.boff[w] + (i - rows); stride = cols;
-  }
+  const SumSpan sp = rowcol_span(p, b);
+  const uint32_t len = sp.len, g0 = sp.g0, stride = sp.stride;
   const uint32_t niter = (len + 63) >> 6;
   X v;
   xyzz_set_inf(v);
@@ -561,21 +592,9 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_quant(MsmPlan p, con
   const uint32_t b = blockIdx.x * MSM_RED_WAVES + (threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
   if (b >= p.nq) return;
-  int w = 0;
-  while (b >= p.qoff[w + 1]) w++;
-  const uint32_t q = b - p.qoff[w];
-  const uint32_t kr = p.kr[w], kc = p.kc[w];
-  const uint32_t rows = 1u << kr, cols = 1u << kc;
-  uint32_t len, bit;
-  const X* src;
-  if (q < kr) {               // U^C_q
-    len = rows; src = rc + p.rcoff[w]; bit = q;
-  } else if (q < kr + kc) {   // U^D_{q-kr}
-    len = cols; src = rc + p.rcoff[w] + rows; bit = q - kr;
-  } else {                    // P
-    len = cols; src = rc + p.rcoff[w] + rows; bit = 32;
-  }
-  const uint32_t niter = (len + 63) >> 6;
+  const QuantSpan qs = quant_span(p, b);
+  const X* src = rc + qs.src;
+  const uint32_t niter = (qs.len + 63) >> 6;
   X v;
   xyzz_set_inf(v);
 #pragma unroll 1
@@ -583,7 +602,7 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_quant(MsmPlan p, con
     X o;
     if (it < niter) {
       const uint32_t t = it * 64 + lane;
-      if (t < len && (bit == 32 || ((t >> bit) & 1))) o = ld_vec(&src[t]);
+      if (quant_has(qs, t)) o = ld_vec(&src[t]);
       else xyzz_set_inf(o);
     } else {
       o = shfl_xor_point(v, 1 << (it - niter));
@@ -635,16 +654,8 @@ __global__ void __launch_bounds__(64 * RW) k_msm_rowcol_q(MsmPlan p, const uint3
   constexpr uint32_t NQ = 16 * RW;
   const uint32_t b = blockIdx.x;
   if (b >= p.nrc) return;   // whole workgroup
-  int w = 0;
-  while (b >= p.rcoff[w + 1]) w++;
-  const uint32_t i = b - p.rcoff[w];
-  const uint32_t rows = 1u << p.kr[w], cols = 1u << p.kc[w];
-  uint32_t len, g0, stride;
-  if (i < rows) {
-    len = cols; g0 = p.boff[w] + i * cols; stride = 1;
-  } else {
-    len = rows; g0 = p.boff[w] + (i - rows); stride = cols;
-  }
+  const SumSpan sp = rowcol_span(p, b);
+  const uint32_t len = sp.len, g0 = sp.g0, stride = sp.stride;
   const uint32_t j = threadIdx.x >> 2;
   const uint32_t niter = (len + NQ - 1) / NQ;
   X v;
@@ -672,22 +683,10 @@ __global__ void __launch_bounds__(64 * RW) k_msm_quant_q(MsmPlan p, const typena
   constexpr uint32_t NQ = 16 * RW;
   const uint32_t b = blockIdx.x;
   if (b >= p.nq) return;
-  int w = 0;
-  while (b >= p.qoff[w + 1]) w++;
-  const uint32_t q = b - p.qoff[w];
-  const uint32_t kr = p.kr[w], kc = p.kc[w];
-  const uint32_t rows = 1u << kr, cols = 1u << kc;
-  uint32_t len, bit;
-  const X* src;
-  if (q < kr) {               // U^C_q
-    len = rows; src = rc + p.rcoff[w]; bit = q;
-  } else if (q < kr + kc) {   // U^D_{q-kr}
-    len = cols; src = rc + p.rcoff[w] + rows; bit = q - kr;
-  } else {                    // P
-    len = cols; src = rc + p.rcoff[w] + rows; bit = 32;
-  }
+  const QuantSpan qs = quant_span(p, b);
+  const X* src = rc + qs.src;
   const uint32_t j = threadIdx.x >> 2;
-  const uint32_t niter = (len + NQ - 1) / NQ;
+  const uint32_t niter = (qs.len + NQ - 1) / NQ;
   X v;
   xyzz_set_inf(v);
 #pragma unroll 1
@@ -696,7 +695,7 @@ __global__ void __launch_bounds__(64 * RW) k_msm_quant_q(MsmPlan p, const typena
     bool have = false;
     if (it < niter) {
       const uint32_t t = it * NQ + j;
-      have = t < len && (bit == 32 || ((t >> bit) & 1));
+      have = quant_has(qs, t);
       if (have) term = ld_vec(&src[t]);
     }
     const X o = quad_sum_step<X, RW>(v, it, niter, xs, have, term);
@@ -721,16 +720,8 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_rowcol_pair(MsmPlan 
   const uint32_t b = blockIdx.x * MSM_RED_WAVES + (threadIdx.x >> 6);
   const uint32_t pr = (threadIdx.x & 63) >> 1;
   if (b >= p.nrc) return;   // whole waves
-  int w = 0;
-  while (b >= p.rcoff[w + 1]) w++;
-  const uint32_t i = b - p.rcoff[w];
-  const uint32_t rows = 1u << p.kr[w], cols = 1u << p.kc[w];
-  uint32_t len, g0, stride;
-  if (i < rows) {
-    len = cols; g0 = p.boff[w] + i * cols; stride = 1;
-  } else {
-    len = rows; g0 = p.boff[w] + (i - rows); stride = cols;
-  }
+  const SumSpan sp = rowcol_span(p, b);
+  const uint32_t len = sp.len, g0 = sp.g0, stride = sp.stride;
   const uint32_t niter = (len + 31) >> 5;
   XYZZ<Fq2h> v;
   xyzz_set_inf(v);
@@ -797,6 +788,68 @@ static uint32_t accum_threads() {
   return T;
 }
 
+// Waves of one row/column-sum launch that the chip holds at once (the
+// kernel's occupancy x CUs), for msm_split_sums.
+template <class C>
+static uint32_t rowcol_waves() {
+  static const uint32_t W = [] {
+    int dev = 0, cus = 0, per_cu = 0;
+    ZK_HIP(hipGetDevice(&dev));
+    ZK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if constexpr (std::is_same<C, G2>::value)
+      ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_rowcol_pair, 64 * MSM_RED_WAVES, 0));
+    else
+      ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_rowcol<C>, 64 * MSM_RED_WAVES, 0));
+    return (uint32_t)std::max(1, per_cu * cus * MSM_RED_WAVES);
+  }();
+  return W;
+}
+
+// Split row/column sums into partial sums (MsmPlan::lsr/lsc) while the
+// launch stays within `target` waves and every partial keeps >= 2 terms per
+// lane group (`lanes` terms per wave step): each wave then runs fewer serial
+// adds before its butterfly, and the waves fill the SIMDs evenly instead of
+// a few long row waves setting the time.  Always the side whose partials are
+// longest first.  The quantities fold the partials with their row's or
+// column's weight.
+// Measured (profiles/r03_ab_split_sums.txt): the standalone 2^20 255-bit G1
+// MSM 3.75 -> 3.64 ms (2^19 buckets: 1536 waves of 22 / 14 steps -> 2048 of
+// 14); the overlapped prove is unchanged by the G1 split (9.62 vs 9.60 ms)
+// and 0.3-0.4 ms SLOWER with the G2 split (its 1024 lane-pair waves crowd the
+// quotient and the A+B1+IC sort, which gate the critical path), so G2 keeps
+// whole sums (ZK_SPLIT_G2=1: A/B build flag).
+#ifndef ZK_SPLIT_G1
+#define ZK_SPLIT_G1 1
+#endif
+#ifndef ZK_SPLIT_G2
+#define ZK_SPLIT_G2 0
+#endif
+static void msm_split_sums(MsmPlan& p, uint32_t target, uint32_t lanes) {
+  auto recount = [&]() {
+    uint32_t rc = 0;
+    for (uint32_t w = 0; w < p.nred; w++) {
+      p.rcoff[w] = rc;
+      rc += (1u << (p.kr[w] + p.lsr[w])) + (1u << (p.kc[w] + p.lsc[w]));
+    }
+    p.rcoff[p.nred] = p.nrc = rc;
+  };
+  for (;;) {
+    int bw = -1;
+    bool brow = false;
+    uint32_t blen = 0;
+    for (uint32_t w = 0; w < p.nred; w++) {
+      const uint32_t rlen = 1u << (p.kc[w] - p.lsr[w]), clen = 1u << (p.kr[w] - p.lsc[w]);
+      if (rlen > blen) { blen = rlen; bw = (int)w; brow = true; }
+      if (clen > blen) { blen = clen; bw = (int)w; brow = false; }
+    }
+    if (bw < 0 || blen / 2 < 2 * lanes) break;
+    const uint32_t add = brow ? 1u << (p.kr[bw] + p.lsr[bw]) : 1u << (p.kc[bw] + p.lsc[bw]);
+    if ((uint64_t)p.nrc + add > target) break;
+    (brow ? p.lsr : p.lsc)[bw]++;
+    recount();
+  }
+}
+
 // Buckets spread over at most this many accumulate chunks are summed by the
 // serial fixup; larger ones go through the log-depth merge.
 constexpr uint32_t MSM_FIX_MAX = 8;
@@ -820,6 +873,10 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
   w.buckets.ensure(sizeof(X) * p.G);
   p.T = accum_threads<C>();
   p.fix_max = MSM_FIX_MAX;
+  // row/column sums: G2 on lane pairs, G1 on lane quads when there are few
+  // (ROWCOL_QUAD_MAX, unsplit), else one lane per add, split to fill the chip
+  const bool quad_rc = !g2 && p.nrc <= ROWCOL_QUAD_MAX;
+  if (!quad_rc && (g2 ? ZK_SPLIT_G2 : ZK_SPLIT_G1)) msm_split_sums(p, rowcol_waves<C>(), g2 ? 32u : 64u);
   w.partials.ensure(sizeof(X) * 2 * (size_t)p.T);
   w.partials2.ensure(sizeof(X) * ((size_t)p.T / 2 + 2));
   w.rc.ensure(sizeof(X) * p.nrc);
@@ -911,7 +968,7 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
   if constexpr (g2)
     k_msm_rowcol_pair<<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(
         p, w.off.as<uint32_t>(), reinterpret_cast<const G2X*>(w.buckets.p), reinterpret_cast<G2X*>(w.rc.p));
-  else if (p.nrc <= ROWCOL_QUAD_MAX)
+  else if (quad_rc)
     k_msm_rowcol_q<C, RW><<<p.nrc, 64 * RW, 0, st>>>(p, w.off.as<uint32_t>(), w.buckets.as<X>(), w.rc.as<X>());
   else
     k_msm_rowcol<C><<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.off.as<uint32_t>(),

@@ -61,7 +61,11 @@ struct MsmPlan {
   uint32_t nb[MSM_MAXWIN];          // buckets in window w (digits 1..nb), a power of two
   uint32_t boff[MSM_MAXWIN + 1];    // first global bucket id of window w
   uint8_t kr[MSM_MAXWIN], kc[MSM_MAXWIN];   // nb = 2^(kr + kc): rows x columns
-  uint32_t rcoff[MSM_MAXWIN + 1];   // first row/col sum of window w (rows, then columns)
+  // each row sum is 2^lsr partial sums over consecutive column ranges, each
+  // column sum 2^lsc over consecutive row ranges (msm_split_sums): rc holds
+  // row i's partial s at i 2^lsr + s, then the columns likewise
+  uint8_t lsr[MSM_MAXWIN], lsc[MSM_MAXWIN];
+  uint32_t rcoff[MSM_MAXWIN + 1];   // first row/col partial sum of window w (rows, then columns)
   uint32_t qoff[MSM_MAXWIN + 1];    // first quantity of window w (U^C, U^D, P)
   uint32_t nred;                    // reduction windows (nwin, or 1 when shared, or nseg)
   int shared;                       // windows share one bucket set (precomputed 2^(c w) P bases)

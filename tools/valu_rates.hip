@@ -38,6 +38,9 @@ __global__ void __launch_bounds__(256) k_rate(const uint32_t* __restrict__ in, u
       if constexpr (OP == 7) asm volatile("v_add_co_u32 %0, vcc, %0, %1" : "+v"(x[i]) : "v"(y) : "vcc");
       if constexpr (OP == 8) asm volatile("v_mad_i64_i32 %0, vcc, %1, %2, %0" : "+v"(acc[i]) : "v"(x[i]), "v"(y) : "vcc");
       if constexpr (OP == 9) asm volatile("v_ashrrev_i64 %0, 28, %0" : "+v"(acc[i]));
+      if constexpr (OP == 10) asm volatile("v_lshrrev_b64 %0, 28, %0" : "+v"(acc[i]));
+      if constexpr (OP == 11) asm volatile("v_and_b32 %0, %0, %1" : "+v"(x[i]) : "v"(y));
+      if constexpr (OP == 12) asm volatile("v_alignbit_b32 %0, %0, %1, 28" : "+v"(x[i]) : "v"(y));
     }
   }
   uint64_t r = 0;
@@ -75,13 +78,14 @@ int main() {
   for (int i = 0; i < 1024; i++) h[i] = 0x9e3779b9u * (i + 1);
   hipMemcpy(in, h, 4096, hipMemcpyHostToDevice);
   const char* names[] = {"v_mad_u64_u32", "v_mul_lo_u32", "v_mul_hi_u32+xor", "v_mad_u32_u24", "v_fma_f64",
-                         "v_lshl_add_u64", "v_add_u32", "v_add_co_u32", "v_mad_i64_i32", "v_ashrrev_i64"};
-  float ms[10] = {run<0>(in, out, blocks), run<1>(in, out, blocks), run<2>(in, out, blocks), run<3>(in, out, blocks),
+                         "v_lshl_add_u64", "v_add_u32", "v_add_co_u32", "v_mad_i64_i32", "v_ashrrev_i64", "v_lshrrev_b64", "v_and_b32", "v_alignbit_b32"};
+  float ms[13] = {run<0>(in, out, blocks), run<1>(in, out, blocks), run<2>(in, out, blocks), run<3>(in, out, blocks),
                   run<4>(in, out, blocks), run<5>(in, out, blocks), run<6>(in, out, blocks), run<7>(in, out, blocks),
-                  run<8>(in, out, blocks), run<9>(in, out, blocks)};
+                  run<8>(in, out, blocks), run<9>(in, out, blocks), run<10>(in, out, blocks), run<11>(in, out, blocks),
+                  run<12>(in, out, blocks)};
   const double ops = (double)blocks * 256 * IT * CH;
   printf("cus %d clock %d MHz\n", cus, clk / 1000);
-  for (int k = 0; k < 10; k++) {
+  for (int k = 0; k < 13; k++) {
     const double rate = ops / (ms[k] * 1e-3);   // lane-ops/s
     const double per_simd_cycle = rate / (cus * 4.0 * clk * 1e3);   // lane-ops per SIMD per cycle
     printf("%-20s %8.3f ms  %7.2f Tlane-op/s  %6.2f lane-op/SIMD/clk  (%.2f cycles per wave64 op)\n", names[k], ms[k],

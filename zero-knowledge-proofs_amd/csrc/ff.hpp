@@ -132,6 +132,32 @@ ZK_DI Fp<P> fp_neg(const Fp<P>& a) { return fp_sub(fp_zero<P>(), a); }
 // -m^-1), so R = 2^(LB NL) (2^392 for Fq, 2^261 for Fr).  Inputs < 2^(32N);
 // output < 2m, reduced once.  Measured 2.1x the 32-bit CIOS on gfx950
 // (tools/mulbench.hip); Fr at 9 x 29 bits: 162 instead of 200 v_mad.
+// Fr column sums in ONE dependency chain (ZK_MAD_CHAIN, default on): every
+// limb product is an inline-asm v_mad whose addend is the running column
+// sum.  Plain C lets LLVM re-associate each column into a chain from 0 plus
+// one v_lshl_add_u64 of the previous column's carry -- a 64-bit add (~5 issue
+// cycles, as many as a v_mad) per column, 17 per Fr product, bought for
+// latency that the NTT's 4 waves/SIMD already hide: 2^22 API NTT 0.554 ->
+// 0.533 ms.  Fq keeps the split columns: its 28-product chains at 3
+// waves/SIMD lost (2^20 MSM 3.61 -> 3.85 ms, prove 9.68 -> 10.13 ms;
+// profiles/r03_ab_mad_chain.txt).
+#ifndef ZK_MAD_CHAIN
+#define ZK_MAD_CHAIN 1
+#endif
+template <bool CH>
+ZK_DI void mad_acc(uint64_t& acc, uint32_t a, uint32_t b) {
+  if constexpr (CH) asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "vcc");
+  else acc += (uint64_t)a * b;
+}
+// b a compile-time constant (modulus limbs): an SGPR operand
+template <bool CH>
+ZK_DI void mad_acc_k(uint64_t& acc, uint32_t a, uint32_t b) {
+  if constexpr (CH) asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(a), "s"(b) : "vcc");
+  else acc += (uint64_t)a * b;
+}
+template <class P>
+constexpr bool mad_chain() { return ZK_MAD_CHAIN && P::NL <= 9; }
+
 template <int N, int M, int LB = 28>
 ZK_DI void unpack28(const uint32_t (&a)[N], uint32_t (&o)[M]) {
   constexpr uint32_t MASK = (1u << LB) - 1;
@@ -169,12 +195,12 @@ ZK_DI Fp<P> fp_mul(const Fp<P>& a, const Fp<P>& b) {
 #pragma unroll
     for (int i = 0; i < M; i++) {
       const int j = k - i;
-      if (j >= 0 && j < M) acc += (uint64_t)x[i] * y[j];
+      if (j >= 0 && j < M) mad_acc<mad_chain<P>()>(acc, x[i], y[j]);
     }
 #pragma unroll
     for (int i = 0; i < M; i++) {
       const int j = k - i;
-      if (i < k && j >= 1 && j < M) acc += (uint64_t)m[i] * P::MODL[j];
+      if (i < k && j >= 1 && j < M) mad_acc_k<mad_chain<P>()>(acc, m[i], P::MODL[j]);
     }
     if (k < M) {
       m[k] = ((uint32_t)acc * P::INVL) & MASK;
@@ -205,14 +231,14 @@ ZK_DI Fp<P> fp_sqr(const Fp<P>& a) {
 #pragma unroll
     for (int i = 0; i < M; i++) {
       const int j = k - i;
-      if (i < j && j < M) cross += (uint64_t)x[i] * x[j];
+      if (i < j && j < M) mad_acc<mad_chain<P>()>(cross, x[i], x[j]);
     }
     uint64_t acc = carry + (cross << 1);
-    if ((k & 1) == 0 && k / 2 < M) acc += (uint64_t)x[k / 2] * x[k / 2];
+    if ((k & 1) == 0 && k / 2 < M) mad_acc<mad_chain<P>()>(acc, x[k / 2], x[k / 2]);
 #pragma unroll
     for (int i = 0; i < M; i++) {
       const int j = k - i;
-      if (i < k && j >= 1 && j < M) acc += (uint64_t)m[i] * P::MODL[j];
+      if (i < k && j >= 1 && j < M) mad_acc_k<mad_chain<P>()>(acc, m[i], P::MODL[j]);
     }
     if (k < M) {
       m[k] = ((uint32_t)acc * P::INVL) & MASK;

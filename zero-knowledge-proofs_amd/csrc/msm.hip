@@ -427,14 +427,27 @@ __device__ __forceinline__ bool big_bucket(const uint32_t* off, uint32_t b, uint
   return (off[b + 1] - 1) / K - off[b] / K + 1 > fix_max;
 }
 
+// One thread per bucket, or -- when there are more buckets than chunks
+// (by_boundary: the 2^19-bucket full-width MSM, where most buckets lie inside
+// one chunk and most per-bucket lanes would idle) one thread per chunk
+// boundary u, which takes the bucket holding entry u K if u is the first
+// boundary inside it.
 template <class C>
-__global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ off, uint32_t G, uint32_t T, uint32_t fix_max,
+__global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ key, const uint32_t* __restrict__ off,
+                                                   uint32_t G, uint32_t T, uint32_t fix_max, bool by_boundary,
                                                    uint32_t* __restrict__ nbig, typename C::X* __restrict__ buckets,
                                                    const typename C::X* __restrict__ partials) {
   using X = typename C::X;
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G) return;
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t K = chunk_len(off[G], T);
+  uint32_t g = u;
+  if (by_boundary) {
+    if (u == 0 || u >= T || (uint64_t)u * K >= off[G]) return;
+    g = key[u * K];
+    if (off[g] / K != u - 1) return;   // not split here, or not its first boundary
+  } else if (g >= G) {
+    return;
+  }
   const uint32_t bs = off[g], be = off[g + 1];
   if (be == bs) return;
   const uint32_t t0 = bs / K, t1 = (be - 1) / K;
@@ -943,8 +956,12 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
         w.off.as<uint32_t>(), p.G, p.T, p.fix_max, w.nbig.as<uint32_t>(), reinterpret_cast<G2X*>(w.buckets.p),
         reinterpret_cast<const G2X*>(w.partials.p));
   else
-    k_msm_fixup<C><<<ceil_div(p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), p.G, p.T, p.fix_max,
-                                                        w.nbig.as<uint32_t>(), w.buckets.as<X>(), w.partials.as<X>());
+  {
+    const bool by_boundary = p.G > p.T;
+    k_msm_fixup<C><<<ceil_div(by_boundary ? p.T : p.G, 128), 128, 0, st>>>(
+        w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T, p.fix_max, by_boundary, w.nbig.as<uint32_t>(),
+        w.buckets.as<X>(), w.partials.as<X>());
+  }
   ZK_LAUNCH_CHECK();
   {
     X* a = w.partials.as<X>();

@@ -629,14 +629,21 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_quant(MsmPlan p, con
 // The same sums with each add split over the 4 lanes of a quad (curve.hpp):
 // one sum per workgroup of RW waves = 16 RW quads.  Quad j folds terms j,
 // j + 16 RW, ... serially, a 4-step __shfl_xor butterfly (lane distances
-// 4..32 keep each lane's quad position) combines a wave, then waves 1..RW-1
-// hand their totals to wave 0 through LDS.  One xyzz_add_quad call site.
-// The quantities (tens of sums) always run on quads; the G1 row/column sums
-// when there are few of them (ROWCOL_QUAD_MAX).  ZK_RED_QWAVES (build flag)
-// waves per quad sum.
+// 4..32 keep each lane's quad position) combines a wave, then a log2(RW)-step
+// tree over LDS combines the waves (wave w + 2^k hands its total to wave w
+// in step k).  One xyzz_add_quad call site.  The quantities (tens of sums)
+// always run on quads, G1 on ZK_QUANT_WAVES_G1 waves per sum (8: two waves
+// per SIMD at 189 VGPRs), G2 on ZK_RED_QWAVES (its 456 VGPRs allow one); the
+// G1 row/column sums when there are few of them (ROWCOL_QUAD_MAX), on
+// ZK_RED_QWAVES waves.
 #ifndef ZK_RED_QWAVES
 #define ZK_RED_QWAVES 4
 #endif
+#ifndef ZK_QUANT_WAVES_G1
+#define ZK_QUANT_WAVES_G1 8
+#endif
+
+constexpr int ilog2_c(int x) { return x <= 1 ? 0 : 1 + ilog2_c(x / 2); }
 
 template <class X, int RW>
 __device__ __forceinline__ X quad_sum_step(X v, uint32_t it, uint32_t niter, X* xs, bool have, const X& term) {
@@ -647,12 +654,11 @@ __device__ __forceinline__ X quad_sum_step(X v, uint32_t it, uint32_t niter, X* 
   } else if (it < niter + 4) {
     o = shfl_xor_point(v, 4 << (it - niter));
   } else {
-    const uint32_t k = it - niter - 4, wave = threadIdx.x >> 6;
-    if (k == 0) {
-      if (wave && (threadIdx.x & 63) == 0) xs[wave - 1] = v;
-      __syncthreads();
-    }
-    if (wave == 0) o = xs[k];
+    const uint32_t k = it - niter - 4, wave = threadIdx.x >> 6, m = 1u << k;
+    __syncthreads();   // the previous step's reads are done
+    if ((wave & (2 * m - 1)) == m && (threadIdx.x & 63) == 0) xs[wave >> (k + 1)] = v;
+    __syncthreads();
+    if ((wave & (2 * m - 1)) == 0) o = xs[wave >> (k + 1)];
     else xyzz_set_inf(o);
   }
   return o;
@@ -663,7 +669,7 @@ __global__ void __launch_bounds__(64 * RW) k_msm_rowcol_q(MsmPlan p, const uint3
                                                          const typename C::X* __restrict__ buckets,
                                                          typename C::X* __restrict__ rc) {
   using X = typename C::X;
-  __shared__ X xs[RW > 1 ? RW - 1 : 1];
+  __shared__ X xs[RW > 1 ? RW / 2 : 1];
   constexpr uint32_t NQ = 16 * RW;
   const uint32_t b = blockIdx.x;
   if (b >= p.nrc) return;   // whole workgroup
@@ -674,7 +680,7 @@ __global__ void __launch_bounds__(64 * RW) k_msm_rowcol_q(MsmPlan p, const uint3
   X v;
   xyzz_set_inf(v);
 #pragma unroll 1
-  for (uint32_t it = 0; it < niter + 4 + (RW - 1); it++) {
+  for (uint32_t it = 0; it < niter + 4 + ilog2_c(RW); it++) {
     X term;
     bool have = false;
     if (it < niter) {
@@ -692,7 +698,7 @@ template <class C, int RW>
 __global__ void __launch_bounds__(64 * RW) k_msm_quant_q(MsmPlan p, const typename C::X* __restrict__ rc,
                                                         typename C::X* __restrict__ res) {
   using X = typename C::X;
-  __shared__ X xs[RW > 1 ? RW - 1 : 1];
+  __shared__ X xs[RW > 1 ? RW / 2 : 1];
   constexpr uint32_t NQ = 16 * RW;
   const uint32_t b = blockIdx.x;
   if (b >= p.nq) return;
@@ -703,7 +709,7 @@ __global__ void __launch_bounds__(64 * RW) k_msm_quant_q(MsmPlan p, const typena
   X v;
   xyzz_set_inf(v);
 #pragma unroll 1
-  for (uint32_t it = 0; it < niter + 4 + (RW - 1); it++) {
+  for (uint32_t it = 0; it < niter + 4 + ilog2_c(RW); it++) {
     X term;
     bool have = false;
     if (it < niter) {
@@ -991,7 +997,8 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
     k_msm_rowcol<C><<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.off.as<uint32_t>(),
                                                                                   w.buckets.as<X>(), w.rc.as<X>());
   ZK_LAUNCH_CHECK();
-  k_msm_quant_q<C, RW><<<p.nq, 64 * RW, 0, st>>>(p, w.rc.as<X>(), w.res.as<X>());
+  constexpr int RWQ = g2 ? ZK_RED_QWAVES : ZK_QUANT_WAVES_G1;
+  k_msm_quant_q<C, RWQ><<<p.nq, 64 * RWQ, 0, st>>>(p, w.rc.as<X>(), w.res.as<X>());
   ZK_LAUNCH_CHECK();
   if (pf) pf->end(st, ph);
 }

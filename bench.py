@@ -275,6 +275,28 @@ def traffic_file(name):
         return None, None
 
 
+def kernel_stats_file(name, prefix):
+    """(calls, total ms) of the kernels whose name starts with `prefix` in a
+    committed rocprofv3 --stats summary (profiles/<name>, the markdown table
+    tools/prof_summary.py writes), else None."""
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    calls, total = 0, 0.0
+    for ln in open(path).read().splitlines()[2:]:
+        c = [x.strip() for x in ln.strip().strip("|").split("|")]
+        if len(c) >= 3 and c[0].startswith(prefix):
+            calls += int(c[1])
+            total += float(c[2])
+    return (calls, total, os.path.relpath(path, ROOT)) if calls else None
+
+
+def ntt_passes(log_n):
+    """Passes of one 2^log_n API transform (ntt.hip pass_plan: the contiguous
+    pass takes up to 11 stages, the rest is split into passes of <= 11)."""
+    return 1 + (max(log_n - 11, 0) + 10) // 11
+
+
 def msm_g1_bench(zkp, ctx, log_n, steps, warmup, seed, cpu=True):
     """configs[1]: G1 MSM, 2^log_n bases, uniform full-width scalars, inputs in HBM."""
     import ctypes as C
@@ -420,14 +442,28 @@ def ntt_bench(zkp, ctx, log_n, steps, warmup, seed, cpu=True):
     k = ctx.profile_read().get("ntt", {"ms": 0.0, "launches": 0})
     ctx.profile(False)
     y = d.cpu().numpy().view(np.uint64).reshape(-1, 4).copy()   # = NTT^steps(x): only the roofline run's state
-    kms = k["ms"] / max(k["launches"], 1)
+    ems = k["ms"] / max(k["launches"], 1)
+    # kernel time per transform from the committed rocprofv3 kernel trace of
+    # tools/ntt_only.py at this size (the pass kernels' total over the
+    # transforms it ran); the live events above bracket whole calls and
+    # include the gaps between the passes' launches
+    ks = kernel_stats_file(f"r03_ntt_2p{log_n}_kernel_stats.md", "k_ntt_pass")
+    if ks:
+        kms = ks[1] / (ks[0] / ntt_passes(log_n))
+        ksrc = f"rocprofv3 --kernel-trace --stats of tools/ntt_only.py {log_n} ({ks[2]}): {ks[0]} pass launches"
+    else:
+        kms = ems
+        ksrc = "HIP events around whole transform calls (no rocprof summary at this size)"
     algo = 2 * 32 * n
     bfly = (n // 2) * log_n
     tmads = bfly * FR_MUL_MADS / (kms / 1e3) / 1e12
     traffic, tsrc = traffic_file(f"pmc_ntt_2p{log_n}.json")
     rec = {"log_n": log_n, "ms_per_ntt": round(dt * 1e3, 3), "elements_per_s": round(n / dt, 1),
            "kernel_ms_per_ntt": round(kms, 4),
-           "kernel_timing": "HIP events around the forward transform's passes on its stream, %d calls" % steps,
+           "kernel_timing": ksrc,
+           "event_ms_per_ntt": round(ems, 4),
+           "event_timing": "HIP events around each forward call on the library's stream, %d calls: the passes plus "
+                           "the launch gaps between them" % steps,
            "api": "zk_ntt_fr_dev (natural order in and out, data in HBM, one stream sync per call)",
            "roundtrip_identity": ok,
            "roofline": {"bound": "hbm", "achieved": round(algo / (kms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,

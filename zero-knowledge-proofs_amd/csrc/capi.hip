@@ -231,7 +231,11 @@ int zk_msm_g2(zk_ctx* ctx, const zk_g2_affine* bases, size_t nb, const zk_fr* sc
 // wider ones -- 13 windows over 2^19 buckets instead of 16 over 2^15: the
 // 2^20 full-width MSM 3.79-3.87 vs 3.92-4.01 ms; c = 18, 19, 22 lose
 // (4.5-5.0 ms; profiles/r02_upload_win_sweep.txt).
-static int upload_win_c(uint32_t win_bits) { return win_bits > 64 ? 20 : 16; }
+// ZK_UPLOAD_WIN_C: A/B variant builds only (tools/build_variant.sh)
+#ifndef ZK_UPLOAD_WIN_C
+#define ZK_UPLOAD_WIN_C 20
+#endif
+static int upload_win_c(uint32_t win_bits) { return win_bits > 64 ? ZK_UPLOAD_WIN_C : 16; }
 
 template <class C, class ABI>
 static int msm_upload(zk_ctx* ctx, const ABI* bases, size_t n, int group, uint32_t win_bits, zk_msm_bases** out) {

@@ -181,13 +181,14 @@ ZK_DI void pack28(const uint32_t (&r)[M], uint32_t (&o)[N]) {
     o[w] = v;
   }
 }
-template <class P>
-ZK_DI Fp<P> fp_mul(const Fp<P>& a, const Fp<P>& b) {
+// The product on operands already cut into limbs.  RED = false skips the
+// final subtraction: the result is then < 2m (inputs < 2^(32N)), which the
+// NTT's tile arithmetic keeps (ntt.hip, fr_*_lz).
+template <class P, bool RED = true>
+ZK_DI Fp<P> fp_mul_limbs(const uint32_t (&x)[P::NL], const uint32_t (&y)[P::NL]) {
   constexpr int N = P::N, M = P::NL, LB = P::LB;
   constexpr uint32_t MASK = (1u << LB) - 1;
-  uint32_t x[M], y[M], m[M], r[M];
-  unpack28<N, M, LB>(a.v, x);
-  unpack28<N, M, LB>(b.v, y);
+  uint32_t m[M], r[M];
   uint64_t carry = 0;
 #pragma unroll
   for (int k = 0; k < 2 * M - 1; k++) {
@@ -213,7 +214,15 @@ ZK_DI Fp<P> fp_mul(const Fp<P>& a, const Fp<P>& b) {
   r[M - 1] = (uint32_t)carry;
   Fp<P> o;
   pack28<N, M, LB>(r, o.v);
-  return fp_reduce_once(o);
+  if constexpr (RED) return fp_reduce_once(o);
+  else return o;
+}
+template <class P, bool RED = true>
+ZK_DI Fp<P> fp_mul(const Fp<P>& a, const Fp<P>& b) {
+  uint32_t x[P::NL], y[P::NL];
+  unpack28<P::N, P::NL, P::LB>(a.v, x);
+  unpack28<P::N, P::NL, P::LB>(b.v, y);
+  return fp_mul_limbs<P, RED>(x, y);
 }
 // Squaring: column k of a^2 is 2 sum_{i<j} a_i a_j (+ a_{k/2}^2), so the
 // product half needs M(M+1)/2 v_mad instead of M^2 (Fq: 105 vs 196); the

@@ -19,6 +19,61 @@ constexpr int NTT_TILE_LOG = ZK_NTT_TILE_LOG;
 #endif
 constexpr int NTT_R = ZK_NTT_R;
 constexpr int NTT_THREADS = (1 << NTT_TILE_LOG) >> NTT_R;
+// Tile arithmetic in [0, 2r) (ZK_NTT_LAZY, default on): products skip their
+// final subtraction (a Montgomery product of inputs < 2^256 is < 2r with
+// R = 2^261), and the butterflies' sums and differences reduce modulo 2r
+// instead of r, which costs the same as the canonical fp_add / fp_sub.  2r <
+// 2^256, so tile values keep the 8-word layout; every pass canonicalises on
+// its store.
+#ifndef ZK_NTT_LAZY
+#define ZK_NTT_LAZY 1
+#endif
+ZK_DI Fr fr_mul_lz(const Fr& a, const Fr& b) { return fp_mul<FrParams, !ZK_NTT_LAZY>(a, b); }
+ZK_DI Fr fr_add_lz(const Fr& a, const Fr& b) {
+  if constexpr (!ZK_NTT_LAZY) return fp_add(a, b);
+  Fr s, t;
+  uint32_t c = 0, bw = 0, k2 = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) s.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t m2 = (FrParams::MOD[i] << 1) | k2;   // 2r, word i (constant-folded)
+    k2 = FrParams::MOD[i] >> 31;
+    t.v[i] = __builtin_subc(s.v[i], m2, bw, &bw);
+  }
+  const bool take_t = c || !bw;   // a + b >= 2r (a carry out means >= 2^256 > 2r)
+#pragma unroll
+  for (int i = 0; i < 8; i++) s.v[i] = take_t ? t.v[i] : s.v[i];
+  return s;
+}
+ZK_DI Fr fr_sub_lz(const Fr& a, const Fr& b) {
+  if constexpr (!ZK_NTT_LAZY) return fp_sub(a, b);
+  Fr d;
+  uint32_t br = 0, c = 0, k2 = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) d.v[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
+  const uint32_t mask = 0u - br;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t m2 = (FrParams::MOD[i] << 1) | k2;
+    k2 = FrParams::MOD[i] >> 31;
+    d.v[i] = __builtin_addc(d.v[i], m2 & mask, c, &c);
+  }
+  return d;
+}
+// [0, 2r) -> canonical
+ZK_DI Fr fr_canon_lz(const Fr& a) {
+  if constexpr (!ZK_NTT_LAZY) return a;
+  return fp_reduce_once(a);
+}
+
+// v * w for a pre-cut twiddle
+ZK_DI Fr fr_mul_wu(const Fr& v, const FrU& w) {
+  uint32_t x[FrParams::NL];
+  unpack28<8, FrParams::NL, FrParams::LB>(v.v, x);
+  return fp_mul_limbs<FrParams, !ZK_NTT_LAZY>(x, w.l);
+}
+
 // One radix-2^R round of a tile's sub-transform: local stages
 // [lsb, lsb + R).  Each thread owns whole groups of 2^R elements (rows
 // r0 + m 2^lsb, one column), keeps them in registers for all R stages and
@@ -26,13 +81,13 @@ constexpr int NTT_THREADS = (1 << NTT_TILE_LOG) >> NTT_R;
 // LDS round trips and 4 barriers instead of 11.  Twiddle of local stage t
 // for row r: omega_(2^(t+1))^(r mod 2^t) = omega_2048^((r mod 2^t) 2^(10-t)).
 template <int R, int Q, bool DIT, bool LSB0>
-__device__ __forceinline__ void ntt_stage(Fr (&x)[1 << R], const Fr* __restrict__ sm, uint32_t rlow, uint32_t lsb) {
+__device__ __forceinline__ void ntt_stage(Fr (&x)[1 << R], const FrU* __restrict__ sm, uint32_t rlow, uint32_t lsb) {
   constexpr int G = 1 << R;
   const uint32_t t = lsb + Q;
   // LSB0 (the round over local stages 0 .. R-1): rlow = 0, so twiddle k of
   // stage Q is omega_2048^(k 2^(10-Q)) and k = 0 is 1 -- those butterflies
   // skip their multiply (all of stage 0, half of stage 1, ...).
-  Fr w[1 << Q];
+  FrU w[1 << Q];
 #pragma unroll
   for (int k = 0; k < (1 << Q); k++)
     if (!(LSB0 && k == 0)) w[k] = ld_vec(&sm[(rlow + ((uint32_t)k << lsb)) << (NTT_SM_LOG - 1 - t)]);
@@ -42,21 +97,21 @@ __device__ __forceinline__ void ntt_stage(Fr (&x)[1 << R], const Fr* __restrict_
     const int k = m & ((1 << Q) - 1);
     Fr u = x[m], v = x[m + (1 << Q)];
     if (LSB0 && k == 0) {
-      x[m] = fp_add(u, v);
-      x[m + (1 << Q)] = fp_sub(u, v);
+      x[m] = fr_add_lz(u, v);
+      x[m + (1 << Q)] = fr_sub_lz(u, v);
     } else if (DIT) {
-      v = fp_mul(v, w[k]);
-      x[m] = fp_add(u, v);
-      x[m + (1 << Q)] = fp_sub(u, v);
+      v = fr_mul_wu(v, w[k]);
+      x[m] = fr_add_lz(u, v);
+      x[m + (1 << Q)] = fr_sub_lz(u, v);
     } else {
-      x[m] = fp_add(u, v);
-      x[m + (1 << Q)] = fp_mul(fp_sub(u, v), w[k]);
+      x[m] = fr_add_lz(u, v);
+      x[m + (1 << Q)] = fr_mul_wu(fr_sub_lz(u, v), w[k]);
     }
   }
 }
 
 template <int R, bool DIT, bool LSB0 = false>
-__device__ __forceinline__ void ntt_round(Fr* sh, const Fr* __restrict__ sm, uint32_t ns, uint32_t logC,
+__device__ __forceinline__ void ntt_round(Fr* sh, const FrU* __restrict__ sm, uint32_t ns, uint32_t logC,
                                           uint32_t lsb) {
   constexpr int G = 1 << R;
   const uint32_t C = 1u << logC;
@@ -85,7 +140,7 @@ __device__ __forceinline__ void ntt_round(Fr* sh, const Fr* __restrict__ sm, uin
 // The rounds of a tile's 2^ns-point sub-transform: DIF top-down (the last
 // round, over local stages 0 .., is the LSB0 one), DIT bottom-up (LSB0 first).
 template <bool DIT>
-__device__ __forceinline__ void ntt_rounds(Fr* sh, const Fr* __restrict__ sm, uint32_t ns, uint32_t logC) {
+__device__ __forceinline__ void ntt_rounds(Fr* sh, const FrU* __restrict__ sm, uint32_t ns, uint32_t logC) {
   const uint32_t full = ns / NTT_R, rem = ns % NTT_R;
   if (DIT) {
     uint32_t lsb = 0;
@@ -178,18 +233,19 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(PassIO io, NttTabs tab
     Fr v = ld_vec(&src[si]);
     if (io.chk && !fr_lt_r(v)) atomicOr(io.chk, 1u);
     if (io.ltab) v = fp_mul(v, ld_vec(&io.ltab[si]));
-    if (DIT && s_lo) v = fp_mul(v, tw_full(tabs, ((lo0 + c) * bitrev32(r, ns)) << tw_shift, log_n));
+    if (DIT && s_lo) v = fr_mul_lz(v, tw_full<!ZK_NTT_LAZY>(tabs, ((lo0 + c) * bitrev32(r, ns)) << tw_shift, log_n));
     st_vec(&sh[k], v);
   }
   __syncthreads();
-  ntt_rounds<DIT>(sh, tabs.sm, ns, logC);
+  ntt_rounds<DIT>(sh, tabs.smu, ns, logC);
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) {
     const uint32_t r = k >> logC, c = k & (C - 1);
     const size_t go = base + ((size_t)r << s_lo) + c;
     Fr v = ld_vec(&sh[k]);
-    if (!DIT && s_lo) v = fp_mul(v, tw_full(tabs, ((lo0 + c) * bitrev32(r, ns)) << tw_shift, log_n));
+    if (!DIT && s_lo) v = fp_mul(v, tw_full<!ZK_NTT_LAZY>(tabs, ((lo0 + c) * bitrev32(r, ns)) << tw_shift, log_n));
     if (io.stab) v = fp_mul(v, ld_vec(&io.stab[go]));
     else if (io.flags & IO_SCALE) v = fp_mul(v, io.scale);
+    else if (DIT || !s_lo) v = fr_canon_lz(v);   // no canonical product above
     st_vec(&dst[go], v);
   }
 }
@@ -309,8 +365,8 @@ void ntt_natural(Fr* dst, const Fr* src, Fr* tmp, const NttDomain& dom, bool inv
 // HBM round trips and the separate scale pass disappear.
 // Batched: the launch covers nb transforms of 2^log_n elements back to back
 // in data (block b works on tile b mod tiles of transform b / tiles).
-__global__ void __launch_bounds__(NTT_THREADS) k_ntt_tile_shift(Fr* __restrict__ data, const Fr* __restrict__ ism,
-                                                               const Fr* __restrict__ sm,
+__global__ void __launch_bounds__(NTT_THREADS) k_ntt_tile_shift(Fr* __restrict__ data, const FrU* __restrict__ ism,
+                                                               const FrU* __restrict__ sm,
                                                                const Fr* __restrict__ tab_br, uint32_t ns,
                                                                uint32_t log_n) {
   extern __shared__ uint4 sh_raw[];
@@ -326,7 +382,8 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_tile_shift(Fr* __restrict__
   }
   __syncthreads();
   ntt_rounds<true>(sh, sm, ns, 0);
-  for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) st_vec(&data[base + k], ld_vec(&sh[k]));
+  for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS)
+    st_vec(&data[base + k], fr_canon_lz(ld_vec(&sh[k])));
 }
 
 void ntt_coset_shift(Fr* d, const NttDomain& dom, const Fr* tab_br, hipStream_t st, Prof* pf, uint32_t nb) {
@@ -345,7 +402,7 @@ void ntt_coset_shift(Fr* d, const NttDomain& dom, const Fr* tab_br, hipStream_t 
     s_hi -= plan[i];
   }
   const uint32_t ns = plan.back();   // s_hi == ns here: the contiguous pass
-  k_ntt_tile_shift<<<(uint32_t)(((uint64_t)nb << L) >> ns), NTT_THREADS, sizeof(Fr) << ns, st>>>(d, ti.sm, tf.sm,
+  k_ntt_tile_shift<<<(uint32_t)(((uint64_t)nb << L) >> ns), NTT_THREADS, sizeof(Fr) << ns, st>>>(d, ti.smu, tf.smu,
                                                                                                 tab_br, ns, L);
   ZK_LAUNCH_CHECK();
   // forward transform: every DIT pass but the first (contiguous) one
@@ -415,6 +472,16 @@ __global__ void k_coset_zinv(Fr* out, uint32_t log_n) {
   *out = acc;
 }
 
+__global__ void __launch_bounds__(256) k_cut_limbs(const Fr* __restrict__ in, FrU* __restrict__ out, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  FrU u;
+  unpack28<8, FrParams::NL, FrParams::LB>(ld_vec(&in[i]).v, u.l);
+#pragma unroll
+  for (int k = 0; k < 12 - FrParams::NL; k++) u.pad[k] = 0;
+  st_vec(&out[i], u);
+}
+
 void ntt_domain_init(NttDomain& d, uint32_t log_n, hipStream_t st) {
   d.log_n = log_n;
   const size_t n = (size_t)1 << log_n;
@@ -436,6 +503,12 @@ void ntt_domain_init(NttDomain& d, uint32_t log_n, hipStream_t st) {
     fr_powers(d.th.as<Fr>(), fr_const(FR_ROOTS[log_n - NTT_TL_LOG]), one, nth, st);
     fr_powers(d.ith.as<Fr>(), fr_const(FR_ROOTS_INV[log_n - NTT_TL_LOG]), one, nth, st);
   }
+  d.smu.ensure(sizeof(FrU) * nsm);
+  d.ismu.ensure(sizeof(FrU) * nsm);
+  k_cut_limbs<<<ceil_div(nsm, 256), 256, 0, st>>>(d.sm.as<Fr>(), d.smu.as<FrU>(), nsm);
+  ZK_LAUNCH_CHECK();
+  k_cut_limbs<<<ceil_div(nsm, 256), 256, 0, st>>>(d.ism.as<Fr>(), d.ismu.as<FrU>(), nsm);
+  ZK_LAUNCH_CHECK();
   d.zinv.ensure(sizeof(Fr));
   k_coset_zinv<<<1, 1, 0, st>>>(d.zinv.as<Fr>(), log_n);
   ZK_LAUNCH_CHECK();

@@ -23,9 +23,17 @@
 namespace zk {
 
 // Per-domain constant tables, built on device once and cached by the ctx.
+// A sub-transform twiddle pre-cut into the product's 9 x 29-bit limbs (the
+// multiply then unpacks only the data operand); 48 B = three 16-B loads.
+struct FrU {
+  uint32_t l[FrParams::NL];
+  uint32_t pad[12 - FrParams::NL];
+};
+
 struct NttDomain {
   uint32_t log_n = 0;
   DevBuf sm, ism;   // omega_2048^j, j < 1024 (and inverse): sub-transform twiddles
+  DevBuf smu, ismu; // the same as FrU (pre-cut limbs)
   DevBuf tl, itl;   // omega_n^x, x < min(n, 4096)
   DevBuf th, ith;   // omega_n^(4096 y), y < n / 4096
   DevBuf zinv;    // (g^n - 1)^-1: 1/Z on the coset g<w>
@@ -59,20 +67,22 @@ ZK_DI uint32_t bitrev32(uint32_t x, uint32_t log_n) {
 
 struct NttTabs {
   const Fr* sm;   // omega_2048^j, j < 1024 (or the inverse root)
+  const FrU* smu; // sm pre-cut into limbs
   const Fr* tl;   // omega_n^x, x < min(n, 4096)
   const Fr* th;   // omega_n^(4096 y), y < n / 4096
 };
 
-// omega_n^x, x < n
+// omega_n^x, x < n (RED = false: < 2r, not canonical)
+template <bool RED = true>
 ZK_DI Fr tw_full(const NttTabs& t, uint32_t x, uint32_t log_n) {
   Fr w = ld_vec(&t.tl[x & ((1u << NTT_TL_LOG) - 1)]);
-  if (log_n > NTT_TL_LOG) w = fp_mul(w, ld_vec(&t.th[x >> NTT_TL_LOG]));
+  if (log_n > NTT_TL_LOG) w = fp_mul<FrParams, RED>(w, ld_vec(&t.th[x >> NTT_TL_LOG]));
   return w;
 }
 
 inline NttTabs tabs_of(const NttDomain& dom, bool inv) {
-  return inv ? NttTabs{dom.ism.as<Fr>(), dom.itl.as<Fr>(), dom.ith.as<Fr>()}
-             : NttTabs{dom.sm.as<Fr>(), dom.tl.as<Fr>(), dom.th.as<Fr>()};
+  return inv ? NttTabs{dom.ism.as<Fr>(), dom.ismu.as<FrU>(), dom.itl.as<Fr>(), dom.ith.as<Fr>()}
+             : NttTabs{dom.sm.as<Fr>(), dom.smu.as<FrU>(), dom.tl.as<Fr>(), dom.th.as<Fr>()};
 }
 
 

@@ -144,6 +144,15 @@ def roofline_from(prof, log_n, overlapped=None):
            "valu": {"achieved_tmad_per_s": round(tmads, 2), "peak_tmad_per_s": VALU_PEAK_TMADS,
                     "frac": round(tmads / VALU_PEAK_TMADS, 4)},
            "note": "integer-VALU bound (381-bit Montgomery products), not HBM; see DESIGN.md"}
+    issue = os.path.join(ROOT, "profiles", "r03_accum_valu_issue.json")
+    if os.path.exists(issue):
+        # SQ_INSTS_VALU pass + measured per-instruction issue costs: how close
+        # the kernel is to the VALU issue limit of its own instruction mix
+        d = json.load(open(issue))
+        out["valu"]["issue"] = {"valu_instr_per_mixed_add": d["valu_wave_instructions_per_mixed_add"],
+                                "v_mad_per_mixed_add": d["v_mad_per_mixed_add"],
+                                "simd_cycles_per_valu_instr": d["simd_cycles_per_valu_instruction"]["no_counters"],
+                                "source": os.path.relpath(issue, ROOT)}
     if overlapped:
         oms, ola, _ = accum(overlapped)
         if ola:

@@ -300,10 +300,15 @@ def kernel_stats_file(name, prefix):
     return (calls, total, os.path.relpath(path, ROOT)) if calls else None
 
 
+NTT_TILE_LOG = 10   # ntt.hip: 2^10-element tiles
+
+
 def ntt_passes(log_n):
     """Passes of one 2^log_n API transform (ntt.hip pass_plan: the contiguous
-    pass takes up to 11 stages, the rest is split into passes of <= 11)."""
-    return 1 + (max(log_n - 11, 0) + 10) // 11
+    pass takes up to NTT_TILE_LOG stages, the rest is split into passes of
+    <= NTT_TILE_LOG)."""
+    t = NTT_TILE_LOG
+    return 1 + (max(log_n - t, 0) + t - 1) // t
 
 
 def msm_g1_bench(zkp, ctx, log_n, steps, warmup, seed, cpu=True):

@@ -47,7 +47,7 @@ def test_ntt_coset_roundtrip(ctx, oracle):
 
 @pytest.mark.parametrize("log_n", [20, 22, 23])
 def test_ntt_roundtrip_large(ctx, oracle, log_n):
-    """2^23: three DIT passes (11 gathered + 6 + 6 stages) on the natural-order path."""
+    """2^23: three DIT passes (10 gathered + 7 + 6 stages) on the natural-order path."""
     x = oracle.random_fr(1 << log_n, 7)
     y = ctx.ntt(x)
     assert np.array_equal(ctx.ntt(y, inverse=True), x)
@@ -78,3 +78,25 @@ def test_ntt_rejects_non_canonical_input(ctx, zkp, oracle, log_n, where):
         assert rc == zkp.ZK_ERR_ARG
     x = oracle.random_fr(n, 6 + log_n)
     assert np.array_equal(ctx.ntt(x), oracle.fft(x))
+
+
+@pytest.mark.parametrize("log_n", [4, 11, 12, 17, 22])
+@pytest.mark.parametrize("kind", ["max", "alt", "two"])
+def test_ntt_extreme_inputs(ctx, oracle, log_n, kind):
+    """Inputs at the top of the field (r - 1 everywhere, r - 1 / 0 alternating,
+    r - 1 / r - 2) push the passes' [0, 2r) tile values (ntt.hip fr_*_lz:
+    products without final subtraction, sums mod 2r with a carry out of 2^256)
+    to their bounds; forward, inverse and coset must still equal the oracle."""
+    R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    n = 1 << log_n
+    lim = lambda v: [(v >> (64 * i)) & (2 ** 64 - 1) for i in range(4)]
+    x = np.zeros((n, 4), dtype=np.uint64)
+    x[:] = lim(R - 1)
+    if kind == "alt":
+        x[1::2] = 0
+    elif kind == "two":
+        x[1::2] = lim(R - 2)
+    assert np.array_equal(ctx.ntt(x), oracle.fft(x))
+    assert np.array_equal(ctx.ntt(x, inverse=True), oracle.fft(x, inverse=True))
+    if log_n <= 17:
+        assert np.array_equal(ctx.ntt(x, coset=7), oracle.coset_fft(x, 7))

@@ -6,10 +6,14 @@
 
 namespace zk {
 
-// 2^NTT_TILE_LOG elements per tile: 2048 x 32 B = 64 KiB of LDS per workgroup
-// (ZK_NTT_TILE_LOG: A/B builds only)
+// 2^NTT_TILE_LOG elements per tile: 1024 x 32 B = 32 KiB of LDS per
+// workgroup (ZK_NTT_TILE_LOG: A/B builds only).  Round 3: 1024-element tiles
+// (256 threads, 5 workgroups per CU instead of 2 x 512 threads) beat 2048
+// once the tile arithmetic went to [0, 2r): 2^22 0.506 -> 0.499 ms with 3
+// passes instead of 2, 2^24 2.35 -> 2.17 ms, 2^20 0.154 -> 0.156 ms
+// (profiles/r03_ab_ntt_tile_radix2.txt)
 #ifndef ZK_NTT_TILE_LOG
-#define ZK_NTT_TILE_LOG 11
+#define ZK_NTT_TILE_LOG 10
 #endif
 constexpr int NTT_TILE_LOG = ZK_NTT_TILE_LOG;
 // Radix of the register rounds (2^NTT_R elements per thread) and threads per
@@ -77,8 +81,8 @@ ZK_DI Fr fr_mul_wu(const Fr& v, const FrU& w) {
 // One radix-2^R round of a tile's sub-transform: local stages
 // [lsb, lsb + R).  Each thread owns whole groups of 2^R elements (rows
 // r0 + m 2^lsb, one column), keeps them in registers for all R stages and
-// touches LDS once per round (16-byte accesses), so an 11-stage tile costs 4
-// LDS round trips and 4 barriers instead of 11.  Twiddle of local stage t
+// touches LDS once per round (16-byte accesses), so a 10-stage tile costs 5
+// LDS round trips and 5 barriers instead of 10.  Twiddle of local stage t
 // for row r: omega_(2^(t+1))^(r mod 2^t) = omega_2048^((r mod 2^t) 2^(10-t)).
 template <int R, int Q, bool DIT, bool LSB0>
 __device__ __forceinline__ void ntt_stage(Fr (&x)[1 << R], const FrU* __restrict__ sm, uint32_t rlow, uint32_t lsb) {
@@ -270,8 +274,9 @@ static void run_pass(bool dit, Fr* d, const NttTabs& t, uint32_t log_n, uint32_t
 }
 
 // Pass plan, top (first DIF pass) to bottom: the contiguous pass (s_lo = 0)
-// takes up to 11 stages; the rest are split evenly into strided passes of
-// <= 11 stages (at 2^22 two passes instead of three: 0.580 vs 0.609 ms with
+// takes up to NTT_TILE_LOG stages; the rest are split evenly into strided
+// passes of <= NTT_TILE_LOG stages (round 2, 2048-element tiles: at 2^22 two
+// passes instead of three, 0.580 vs 0.609 ms with
 // depth 9, profiles/r02_ntt_sweep.txt; a one-column tile's 32-byte rows share
 // lines with its neighbours, which the XCD-aware tile order keeps in one L2).
 static uint32_t max_strided() { return NTT_TILE_LOG; }

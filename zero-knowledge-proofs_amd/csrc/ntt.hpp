@@ -8,7 +8,7 @@
 //
 // Layout: Fr elements are 32 B (8 x u32 Montgomery limbs), contiguous.
 // Four-step (recursive) structure: a pass loads a tile of 2^ns rows x C
-// consecutive columns into LDS (<= 2048 elements = 64 KiB), runs the
+// consecutive columns into LDS (<= 1024 elements = 32 KiB), runs the
 // 2^ns-point sub-transform down its columns with twiddles from a small
 // cached table, and applies the inter-level twiddles once per element, so
 // log n stages cost ~log n / 10 HBM round trips and no per-butterfly

@@ -315,6 +315,14 @@ int zk_ctx_attach_exchange(zk_ctx *ctx, const zk_exchange_ops *ops, int rank, in
 int zk_test_prove_virtual_shards(zk_ctx *ctx, const zk_pk_dev *const *shards, uint32_t nshards,
                                  const void *d_z, size_t zlen, size_t num_public, const zk_fr *r,
                                  const zk_fr *s, zk_proof *out);
+/* Diagnostic: the attached exchange's two operations on their own, on the
+ * ctx's stream -- one all-to-all of chunk_bytes per rank over a device
+ * buffer whose chunk k holds bytes (rank * 31 + k * 7 + i) & 0xff, then the
+ * status agreement of `status`.  *out_max = the agreed maximum; ZK_OK when
+ * every received chunk s equals what rank s sent, ZK_ERR_RCCL otherwise (or
+ * on a transport error).  Runs ncclAllToAll / ncclAllReduce themselves on a
+ * world-1 RCCL communicator, where a one-GPU box can reach them. */
+int zk_test_exchange(zk_ctx *ctx, size_t chunk_bytes, int32_t status, int32_t *out_max);
 
 /* ---------------------------------------------------------------- QAP --- */
 /* QAP::evaluate_at (crates/groth16-qap/src/lib.rs:190-220): out[0..2] =

@@ -55,6 +55,9 @@ def _worker(rank, world, port, log_n, seed, out_dir, fault):
     r, s = rng.fr(), rng.fr()
     ctx = zkp.Context(0)
     ctx.attach_exchange(zkp.TorchExchange(), rank, world)
+    # the exchange's two operations alone (zk_test_exchange): rank-tagged
+    # chunks through one all-to-all, then the status agreement
+    res["exchange_max"] = ctx.test_exchange(4099, 3 * rank)
     qap = zkp.QAP(zkp.CSRMatrices.synthetic(n))
     dpk = zkp.CRS.generate_device(ctx, qap, zkp.SetupParams(*params), 1, shard=rank, nshards=world)
     z = oracle.synthetic_witness(n, seed + 1)
@@ -119,6 +122,7 @@ def test_host_exchange_sliced_witness_matches_oracle(oracle, tmp_path, world):
     res = _run(tmp_path, world, log_n, seed, False)
     assert res[0]["proof"] == _oracle_proof(oracle, log_n, seed)
     for r in res:
+        assert r["exchange_max"] == 3 * (world - 1)
         assert r["device_partial_equal"]
         # z_0 plus this rank's rows' variables: ~1/N of the witness
         assert r["slice_rows"] <= r["zlen"] // world + 2, r

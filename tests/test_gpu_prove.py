@@ -148,11 +148,16 @@ def test_distributed_quotient_rejects_bad_witness(ctx, zkp, oracle):
 
 def test_rccl_attach_single_rank(zkp):
     """The library's RCCL communicator (used by sharded keys' distributed
-    quotient) initialises through the C ABI; world 1 needs no peers."""
+    quotient) initialises through the C ABI; world 1 needs no peers.  On it,
+    the exchange's own collectives run: ncclAllToAll of one chunk (odd and
+    large sizes) and the ncclAllReduce(max) status agreement, both on the
+    ctx's stream -- the calls the 8-GPU distributed quotient makes."""
     uid = zkp.Context.rccl_unique_id()
     assert len(uid) == 128
     with zkp.Context(0) as c:
         c.attach_rccl(uid, 0, 1)
+        for chunk, status in ((1, 0), (37, 5), (3 << 20, -2), (96 << 20, 7)):
+            assert c.test_exchange(chunk, status) == status
 
 
 def test_prove_all_ones_witness(ctx, zkp, oracle):

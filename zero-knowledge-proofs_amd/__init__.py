@@ -49,6 +49,7 @@ EXPORTS = (
     "zk_msm_g2_upload_windows", "zk_build_id", "zk_ctx_set_schedule", "zk_qap_evaluate_at",
     "zk_poly_evaluate_batch", "zk_synthetic_witness_dev", "zk_ctx_set_option", "zk_ctx_timeline_read",
     "zk_ctx_attach_exchange", "zk_groth16_witness_ranges", "zk_groth16_prove_partial_host",
+    "zk_test_exchange",
 )
 ZK_OPT_QUOTIENT_PATH, ZK_OPT_PROVE_WIN_C, ZK_OPT_EXCHANGE_TIMEOUT_MS, ZK_OPT_FAULT_AFTER_EXCHANGE = 1, 2, 3, 4
 CSRC = os.path.join(_HERE, "csrc")
@@ -290,6 +291,15 @@ class Context:
         buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
         _check(lib().zk_ctx_attach_rccl(C.c_void_p(self._h), buf, C.c_int(rank), C.c_int(world)), self,
                "zk_ctx_attach_rccl")
+
+    def test_exchange(self, chunk_bytes, status):
+        """zk_test_exchange: one all-to-all and one status agreement on the
+        attached exchange (RCCL or host-staged); returns the agreed max,
+        raises ExchangeError when a received chunk is wrong."""
+        out = C.c_int32()
+        _check(lib().zk_test_exchange(C.c_void_p(self._h), C.c_size_t(chunk_bytes), C.c_int32(status),
+                                      C.byref(out)), self, "zk_test_exchange")
+        return out.value
 
     def attach_exchange(self, exchange, rank, world):
         """zk_ctx_attach_exchange: the distributed quotient of sharded keys

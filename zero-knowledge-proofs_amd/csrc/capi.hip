@@ -561,6 +561,31 @@ int zk_test_prove_virtual_shards(zk_ctx* ctx, const zk_pk_dev* const* shards, ui
   ZK_GUARD(ctx, { return prove_virtual_shards_impl(ctx, shards, nshards, d_z, zlen, num_public, r, s, out); })
 }
 
+int zk_test_exchange(zk_ctx* ctx, size_t chunk_bytes, int32_t status, int32_t* out_max) {
+  if (!ctx || !out_max || !chunk_bytes || chunk_bytes > ((size_t)1 << 30)) return ZK_ERR_ARG;
+  ZK_GUARD(ctx, {
+    if (!ctx->exch) throw Error(ZK_ERR_ARG, "test_exchange: no exchange attached");
+    Exchange& ex = *ctx->exch;
+    const size_t W = (size_t)ex.world, bytes = chunk_bytes * W;
+    std::vector<uint8_t> h(bytes);
+    for (size_t k = 0; k < W; k++)
+      for (size_t i = 0; i < chunk_bytes; i++) h[k * chunk_bytes + i] = (uint8_t)((ex.rank * 31 + k * 7 + i) & 0xff);
+    DevBuf send, recv;
+    send.ensure(bytes);
+    recv.ensure(bytes);
+    ZK_HIP(hipMemcpyAsync(send.p, h.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
+    ZK_HIP(hipMemsetAsync(recv.p, 0, bytes, ctx->stream));
+    ex.all_to_all(send.p, recv.p, chunk_bytes, ctx->stream);
+    *out_max = ex.agree_max(status, ctx->stream);
+    ZK_HIP(hipMemcpyAsync(h.data(), recv.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    ZK_HIP(hipStreamSynchronize(ctx->stream));
+    for (size_t s = 0; s < W; s++)   // chunk s came from rank s, which filled its chunk `rank` for us
+      for (size_t i = 0; i < chunk_bytes; i++)
+        if (h[s * chunk_bytes + i] != (uint8_t)((s * 31 + (size_t)ex.rank * 7 + i) & 0xff)) return ZK_ERR_RCCL;
+    return ZK_OK;
+  })
+}
+
 int zk_proof_serialize_compressed(const zk_proof* proof, uint8_t out[192]) {
   if (!proof || !out) return ZK_ERR_ARG;
   serialize_g1_compressed(proof->a, out);

@@ -498,9 +498,13 @@ static const int G1_ABI[3] = {MSM_A, MSM_B1, MSM_IC};
 // already on the device, with the witness-check flags of all ranks.
 // ranges: only these [lo, hi) entries of d_z are valid (a witness slice),
 // else all of [0, V).
+// early (the one-GPU prove): pi_A and pi_B in their affine ABI form as soon
+// as those MSMs are done, while H is still on the GPU -- each conversion is
+// a field inversion (~40 us on one core) that would otherwise follow the
+// last MSM.
 static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, const zk_fr* r,
                              const zk_fr* s, const uint64_t* h_given = nullptr, uint32_t given_flags = 0,
-                             const std::vector<uint64_t>* ranges = nullptr) {
+                             const std::vector<uint64_t>* ranges = nullptr, zk_proof* early = nullptr) {
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
   const auto t_start = clk::now();
@@ -638,6 +642,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       const auto t_f = clk::now();
       if (slot == MSM_B2) {
         p.B2 = msm_finish<G2>(ctx->msm[slot]);
+        if (early) host_to_abi<G2>(p.B2, reinterpret_cast<uint64_t*>(&early->b));
       } else if (slot == MSM_A) {
         p.A = msm_finish_seg<G1>(ctx->msm[slot], 0);
         p.B1 = msm_finish_seg<G1>(ctx->msm[slot], 1);
@@ -650,6 +655,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       left--;
       if (!sc_done && ab_done) {
         p.SC = host::mul2_scalar(p.A, s->l, p.B1, r->l);
+        if (early) host_to_abi<G1>(p.A, reinterpret_cast<uint64_t*>(&early->a));
         sc_done = true;
       }
       t_fin += ms_since(t_f);
@@ -700,8 +706,14 @@ int prove_impl(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, size_t zlen, s
   if (num_public >= zlen) return ZK_ERR_INVALID_WITNESS;
   if (zlen != pk->V) return ZK_ERR_INVALID_WITNESS;
   if (pk->nshards != 1) return ZK_ERR_ARG;
-  Partial p = prove_partial(ctx, pk, reinterpret_cast<const uint64_t*>(d_z), r, s);
-  return combine(&p, 1, out);
+  zk_proof ab{};
+  Partial p = prove_partial(ctx, pk, reinterpret_cast<const uint64_t*>(d_z), r, s, nullptr, 0, nullptr, &ab);
+  if (p.status != ZK_OK) return p.status;
+  // combine() for one part: pi_A, pi_B already converted; pi_C = IC + H + s A + r B1
+  out->a = ab.a;
+  out->b = ab.b;
+  host_to_abi<G1>(host::addp(host::addp(p.IC, p.H), p.SC), reinterpret_cast<uint64_t*>(&out->c));
+  return ZK_OK;
 }
 
 // z_host / ranges: a host witness slice (zk_groth16_prove_partial_host) to

@@ -228,7 +228,6 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(PassIO io, NttTabs tab
   const uint32_t hi = tile / lo_blocks;
   const uint32_t lo0 = (tile % lo_blocks) << logC;
   const size_t base = ((size_t)hi << (s_lo + ns)) + lo0;
-  const uint32_t tw_shift = log_n - s_lo - ns;          // omega_N = omega_n^(2^tw_shift)
 
   for (uint32_t k = threadIdx.x; k < tile_elems; k += NTT_THREADS) {
     const uint32_t r = k >> logC, c = k & (C - 1);
@@ -237,7 +236,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(PassIO io, NttTabs tab
     Fr v = ld_vec(&src[si]);
     if (io.chk && !fr_lt_r(v)) atomicOr(io.chk, 1u);
     if (io.ltab) v = fp_mul(v, ld_vec(&io.ltab[si]));
-    if (DIT && s_lo) v = fr_mul_lz(v, tw_full<!ZK_NTT_LAZY>(tabs, ((lo0 + c) * bitrev32(r, ns)) << tw_shift, log_n));
+    if (DIT && s_lo) v = fr_mul_lz(v, tw_pass<!ZK_NTT_LAZY>(tabs, (lo0 + c) * bitrev32(r, ns), s_lo + ns, log_n));
     st_vec(&sh[k], v);
   }
   __syncthreads();
@@ -246,7 +245,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(PassIO io, NttTabs tab
     const uint32_t r = k >> logC, c = k & (C - 1);
     const size_t go = base + ((size_t)r << s_lo) + c;
     Fr v = ld_vec(&sh[k]);
-    if (!DIT && s_lo) v = fp_mul(v, tw_full<!ZK_NTT_LAZY>(tabs, ((lo0 + c) * bitrev32(r, ns)) << tw_shift, log_n));
+    if (!DIT && s_lo) v = fp_mul(v, tw_pass<!ZK_NTT_LAZY>(tabs, (lo0 + c) * bitrev32(r, ns), s_lo + ns, log_n));
     if (io.stab) v = fp_mul(v, ld_vec(&io.stab[go]));
     else if (io.flags & IO_SCALE) v = fp_mul(v, io.scale);
     else if (DIT || !s_lo) v = fr_canon_lz(v);   // no canonical product above
@@ -507,6 +506,17 @@ void ntt_domain_init(NttDomain& d, uint32_t log_n, hipStream_t st) {
   if (log_n > NTT_TL_LOG) {   // omega_n^4096 = omega_(n / 4096)
     fr_powers(d.th.as<Fr>(), fr_const(FR_ROOTS[log_n - NTT_TL_LOG]), one, nth, st);
     fr_powers(d.ith.as<Fr>(), fr_const(FR_ROOTS_INV[log_n - NTT_TL_LOG]), one, nth, st);
+  }
+  if (log_n > NTT_TL_LOG && NTT_TS_LOG > NTT_TL_LOG) {
+    // direct twiddles for the passes over blocks of <= 2^16 (round 3): one
+    // L2-resident load instead of TL x TH, a load and a product less per
+    // element (2^22 API NTT: the first strided pass)
+    d.ts_log = std::min<uint32_t>(log_n, NTT_TS_LOG);
+    const size_t nts = (size_t)1 << d.ts_log;
+    d.ts.ensure(sizeof(Fr) * nts);
+    d.its.ensure(sizeof(Fr) * nts);
+    fr_powers(d.ts.as<Fr>(), fr_const(FR_ROOTS[d.ts_log]), one, nts, st);
+    fr_powers(d.its.as<Fr>(), fr_const(FR_ROOTS_INV[d.ts_log]), one, nts, st);
   }
   d.smu.ensure(sizeof(FrU) * nsm);
   d.ismu.ensure(sizeof(FrU) * nsm);

@@ -36,6 +36,8 @@ struct NttDomain {
   DevBuf smu, ismu; // the same as FrU (pre-cut limbs)
   DevBuf tl, itl;   // omega_n^x, x < min(n, 4096)
   DevBuf th, ith;   // omega_n^(4096 y), y < n / 4096
+  DevBuf ts, its;   // omega_S^e, e < S = 2^min(16, log n) (log n > 12): cache-resident direct twiddles
+  uint32_t ts_log = 0;
   DevBuf zinv;    // (g^n - 1)^-1: 1/Z on the coset g<w>
   // n-entry coset tables, built on first use only (n x 32 B each: 512 MB at
   // 2^24), so API-only transforms build none and each quotient path builds
@@ -52,6 +54,10 @@ const Fr* domain_gipow(NttDomain& d, hipStream_t st);
 
 constexpr int NTT_SM_LOG = 11;    // sub-transform twiddles: powers of omega_2048 (domain-independent)
 constexpr int NTT_TL_LOG = 12;    // omega_n^x = TL[x mod 4096] * TH[x / 4096]
+#ifndef ZK_NTT_TS_LOG
+#define ZK_NTT_TS_LOG 16
+#endif
+constexpr uint32_t NTT_TS_LOG = ZK_NTT_TS_LOG;   // direct pass-twiddle table: 2^16 x 32 B = 2 MB (A/B: 0 = none)
 
 // a (8 little-endian u32 limbs, as stored) < r: a canonical Fr
 ZK_DI bool fr_lt_r(const Fr& a) {
@@ -70,8 +76,16 @@ struct NttTabs {
   const FrU* smu; // sm pre-cut into limbs
   const Fr* tl;   // omega_n^x, x < min(n, 4096)
   const Fr* th;   // omega_n^(4096 y), y < n / 4096
+  const Fr* ts;   // omega_S^e, e < S = 2^ts_log (nullptr: none)
+  uint32_t ts_log;
 };
 
+// The inter-level twiddle of a pass over blocks of N = 2^logN elements:
+// omega_N^x, x < N.  With N <= S it is ONE load from the direct table
+// (omega_S^(x 2^(ts_log - logN)): 2 MB at S = 2^16, L2-resident), else
+// TL x TH below (RED = false: < 2r, not canonical).
+template <bool RED = true>
+ZK_DI Fr tw_pass(const NttTabs& t, uint32_t x, uint32_t logN, uint32_t log_n);
 // omega_n^x, x < n (RED = false: < 2r, not canonical)
 template <bool RED = true>
 ZK_DI Fr tw_full(const NttTabs& t, uint32_t x, uint32_t log_n) {
@@ -80,9 +94,17 @@ ZK_DI Fr tw_full(const NttTabs& t, uint32_t x, uint32_t log_n) {
   return w;
 }
 
+template <bool RED>
+ZK_DI Fr tw_pass(const NttTabs& t, uint32_t x, uint32_t logN, uint32_t log_n) {
+  if (t.ts && logN <= t.ts_log) return ld_vec(&t.ts[x << (t.ts_log - logN)]);
+  return tw_full<RED>(t, x << (log_n - logN), log_n);
+}
+
 inline NttTabs tabs_of(const NttDomain& dom, bool inv) {
-  return inv ? NttTabs{dom.ism.as<Fr>(), dom.ismu.as<FrU>(), dom.itl.as<Fr>(), dom.ith.as<Fr>()}
-             : NttTabs{dom.sm.as<Fr>(), dom.smu.as<FrU>(), dom.tl.as<Fr>(), dom.th.as<Fr>()};
+  return inv ? NttTabs{dom.ism.as<Fr>(), dom.ismu.as<FrU>(), dom.itl.as<Fr>(), dom.ith.as<Fr>(), dom.its.as<Fr>(),
+                       dom.ts_log}
+             : NttTabs{dom.sm.as<Fr>(), dom.smu.as<FrU>(), dom.tl.as<Fr>(), dom.th.as<Fr>(), dom.ts.as<Fr>(),
+                       dom.ts_log};
 }
 
 

@@ -148,12 +148,16 @@ int zk_ctx_set_schedule(zk_ctx *ctx, int schedule);
  *                         60000, >= 1): a distributed-quotient proof whose
  *                         peers do not answer within it fails with
  *                         ZK_ERR_RCCL and aborts the exchange
- *   ZK_OPT_FAULT_AFTER_EXCHANGE  test hook, 0 (default) or 1..3: the next
- *                         distributed-quotient proof on this ctx fails right
- *                         after its k-th all-to-all, as a rank-local error
- *                         would (tests of the abort path) */
+ *   ZK_OPT_DIST_QUOTIENT  -1 (default): a sharded key's quotient is
+ *                         distributed whenever the ctx has an exchange of the
+ *                         key's (shard, nshards) attached; 0: never -- every
+ *                         rank computes the whole quotient and reads the
+ *                         whole witness (the replicated alternative, for
+ *                         measuring one against the other on one node)
+ * (Test hooks -- the virtual-rank prove, the bare exchange, fault injection
+ * -- live in a separate library, include/zkp_test.h.) */
 enum { ZK_OPT_QUOTIENT_PATH = 1, ZK_OPT_PROVE_WIN_C = 2, ZK_OPT_EXCHANGE_TIMEOUT_MS = 3,
-       ZK_OPT_FAULT_AFTER_EXCHANGE = 4 };
+       ZK_OPT_DIST_QUOTIENT = 5 };
 int zk_ctx_set_option(zk_ctx *ctx, int option, int64_t value);
 
 /* ---------------------------------------------------------------- MSM --- */
@@ -265,15 +269,20 @@ int zk_groth16_prove_partial(zk_ctx *ctx, const zk_pk_dev *pk_shard, const void 
  * index ranges [ranges[2k], ranges[2k+1]) of z, ascending and disjoint (at
  * most cap are written).  With a distributed quotient (an exchange of the
  * key's shape attached) that is z_0, the variables of the shard's MSM bases
- * and those its quotient rows reference -- about 2/N of the witness for N
- * shards; otherwise all of [0, zlen).  No reference counterpart. */
+ * and those its quotient rows reference, plus the variables var_owner gives
+ * the shard (so every z entry is read, and checked canonical, by some rank)
+ * -- 1/N of the witness plus z_0 for the synthetic circuit (3n/N + 1
+ * entries), since a shard's MSM variables are those its quotient rows first
+ * reference; otherwise all of [0, zlen).  No reference counterpart. */
 int zk_groth16_witness_ranges(zk_ctx *ctx, const zk_pk_dev *pk_shard, uint64_t *ranges, size_t cap,
                               size_t *nranges);
 /* zk_groth16_prove_partial from a HOST witness slice -- the sharded form of
  * the drop-in prove(pk, witness, rng) (crates/groth16-core/src/lib.rs:139-147),
  * each rank receiving only its part: z_slice holds z[lo..hi) of every range
  * of zk_groth16_witness_ranges, concatenated in order (slice_len entries in
- * all, else ZK_ERR_ARG); zlen is the length of the whole witness (the
+ * all, else ZK_ERR_ARG -- with a distributed quotient on every rank at once,
+ * through the ranks' status agreement, so no peer is left waiting in an
+ * all-to-all); zlen is the length of the whole witness (the
  * Witness::validate length check, core:113-118). */
 int zk_groth16_prove_partial_host(zk_ctx *ctx, const zk_pk_dev *pk_shard, const zk_fr *z_slice,
                                   size_t slice_len, size_t zlen, size_t num_public, const zk_fr *r,
@@ -309,21 +318,6 @@ typedef struct {
   void *user;
 } zk_exchange_ops;
 int zk_ctx_attach_exchange(zk_ctx *ctx, const zk_exchange_ops *ops, int rank, int world);
-/* Diagnostic: nshards virtual ranks of one key on this ctx's single device
- * (the all-to-alls become device copies) -- checks the distributed path's
- * arithmetic and index maps without N devices. */
-int zk_test_prove_virtual_shards(zk_ctx *ctx, const zk_pk_dev *const *shards, uint32_t nshards,
-                                 const void *d_z, size_t zlen, size_t num_public, const zk_fr *r,
-                                 const zk_fr *s, zk_proof *out);
-/* Diagnostic: the attached exchange's two operations on their own, on the
- * ctx's stream -- one all-to-all of chunk_bytes per rank over a device
- * buffer whose chunk k holds bytes (rank * 31 + k * 7 + i) & 0xff, then the
- * status agreement of `status`.  *out_max = the agreed maximum; ZK_OK when
- * every received chunk s equals what rank s sent, ZK_ERR_RCCL otherwise (or
- * on a transport error).  Runs ncclAllToAll / ncclAllReduce themselves on a
- * world-1 RCCL communicator, where a one-GPU box can reach them. */
-int zk_test_exchange(zk_ctx *ctx, size_t chunk_bytes, int32_t status, int32_t *out_max);
-
 /* ---------------------------------------------------------------- QAP --- */
 /* QAP::evaluate_at (crates/groth16-qap/src/lib.rs:190-220): out[0..2] =
  * A(point), B(point), C(point) = sum_i z_i A_i(point) etc., out[3] = Z(point)

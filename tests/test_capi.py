@@ -6,10 +6,11 @@ import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 HEADER = os.path.join(HERE, "..", "include", "zkp.h")
+TEST_HEADER = os.path.join(HERE, "..", "include", "zkp_test.h")
 
 
-def declared():
-    src = open(HEADER).read()
+def declared(header=HEADER):
+    src = open(header).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(zk_[a-z0-9_]+)\s*\(", src)))
 
@@ -24,6 +25,19 @@ def test_library_exports_every_symbol(zkp):
     missing = [n for n in declared() if not hasattr(lib, n)]
     assert not missing, missing
     assert sorted(zkp.EXPORTS) == declared()
+
+
+def test_test_hooks_live_in_their_own_library(zkp):
+    """zk_test_* (virtual ranks, bare exchange, fault injection) are declared
+    in include/zkp_test.h and exported by libzkp_amd_test.so only: the
+    shipped library has no way to inject a failure."""
+    lib = ctypes.CDLL(zkp.LIB_PATH)
+    for n in declared(TEST_HEADER):
+        assert not hasattr(lib, n), n
+    assert sorted(zkp.TEST_EXPORTS) == declared(TEST_HEADER)
+    t = zkp.test_lib()
+    for n in zkp.TEST_EXPORTS:
+        assert hasattr(t, n)
 
 
 def test_struct_sizes(zkp):

@@ -28,10 +28,6 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 LOG_N = 24
-ORACLE_2P24 = ("975ca696ac5acaa2c7690b9d89ab763ee435fdae4fa76daf9d90e40e6c4cef0407dec0cf4b602165b475c26696cbec3e"
-               "a7ab7a7b36fda6704c05a6dedbb181099f278a050b96ebd2862da2a29bb0b436efb8cb355c2bb4c889dd0089e68a7d45"
-               "13db14b6f7322595e922f20c068400f5a044f3a4ce7311fec64d1f7e76ea24d68c1dd5328373c7369b56bd414eb6dea3"
-               "9583f11348f3813b597738ee46c4145abb606199f147e04bf4786b7fbe29b7e9646516e5f7dedf4535783d11ece4d9ce")
 
 
 def _bench():
@@ -57,7 +53,7 @@ def case_2p24(ctx, zkp, oracle):
     del opk
     assert rc == 0
     print(f"\n[2^24] oracle proof on {oracle.default_threads()} threads: {time.perf_counter() - t:.1f} s", flush=True)
-    assert oracle.proof_compress(oproof).hex() == ORACLE_2P24
+    assert oracle.proof_compress(oproof).hex() == bench.ORACLE_2P24   # the bytes bench.py's anchor is checked against
     return qap, params, r, s, z, oproof
 
 
@@ -101,3 +97,16 @@ def test_2p24_eight_shards_virtual_and_partial(ctx, zkp, case_2p24):
             d.free()
     print(f"[2^24 x 8 shards] GPU setup {t_setup:.2f} s, virtual-rank proof {t_v * 1e3:.0f} ms, "
           f"8 partials (replicated quotient) {t_p * 1e3:.0f} ms", flush=True)
+
+
+@pytest.mark.timeout(600)
+def test_bench_anchor_matches_pinned_oracle_proof(ctx, zkp, case_2p24):
+    """bench.py's N = 1 strong-scaling anchor (configs[4] on one GPU) checks
+    its proof against bench.ORACLE_2P24; the fixture above pinned those bytes
+    to a fresh oracle run."""
+    bench = _bench()
+    params, r, s = bench.setup_params(bench.DEFAULT_SEED)
+    rec = bench.anchor_bench(zkp, ctx, LOG_N, params, r, s, bench.DEFAULT_SEED, 1, 0)
+    assert rec["bit_exact_vs_oracle"] is True
+    assert rec["msm_only"]["ms_per_step"] > 0 and rec["roofline"]["avg_launch_ms"] > 0
+    print(f"[2^24 anchor] {rec['ms_per_step']} ms, MSM kernels {rec['msm_only']['ms_per_step']} ms", flush=True)

@@ -34,7 +34,7 @@ def test_bench_two_rank_path_matches_single_gpu(ctx, zkp):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
-           "--total-log-n", str(log_n), "--seed", str(seed)]
+           "--total-log-n", str(log_n), "--seed", str(seed), "--cpu-sample-log-n", "10"]
     res = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=280)
     assert res.returncode == 0, res.stderr[-3000:]
     line = [ln for ln in res.stdout.splitlines() if ln.startswith("{")][-1]
@@ -43,6 +43,17 @@ def test_bench_two_rank_path_matches_single_gpu(ctx, zkp):
     assert rec["config"]["constraints"] == 1 << log_n and rec["config"]["quotient"] == "distributed-host"
     pc = rec["pcie_inclusive"]
     assert pc["max_rank_witness_bytes"] <= pc["witness_bytes"] // 2 + 64
+    # the fields that make the driver's 1 -> 8 GPU run readable as a curve
+    # (DESIGN.md 5): the MSMs' own time, the dominant kernel's roofline, the
+    # replicated-quotient alternative on the same keys, a CPU baseline
+    mo = rec["msm_only"]
+    assert 0 < mo["ms_per_step"] <= rec["serial_schedule"]["ms_per_step"]
+    assert mo["pairs_per_s"] > 0 and mo["g1_pairs"] == 10 * (1 << log_n) + 6
+    roof = rec["roofline"]
+    assert roof["kernel"] == "k_msm_accum<G1>" and 0 < roof["frac"] < 1 and roof["avg_launch_ms"] > 0
+    assert rec["quotient_replicated"]["ms_per_step"] > 0
+    cb = rec["cpu_baseline"]
+    assert cb["value"] > 0 and cb["bit_exact_vs_gpu"] and cb["cores"] >= 1
     sys.path.insert(0, ROOT)
     import bench
     params, r, s = bench.setup_params(seed)

@@ -11,10 +11,17 @@ the 8-GPU run takes (only ncclAllToAll itself differs).
     in one all-gather and the folded proof equals the C oracle's;
   * the device-witness partial (zk_groth16_prove_partial) equals the
     host-slice one byte for byte;
-  * a rank that fails mid-quotient (ZK_OPT_FAULT_AFTER_EXCHANGE: right after
-    the 2nd all-to-all) aborts the exchange: it returns its error, its peer
-    -- blocked in the 3rd all-to-all -- returns ZK_ERR_RCCL instead of
-    hanging, and the aborted exchange refuses further proofs."""
+  * a rank that fails mid-quotient (zk_test_fault_after_exchange, from the
+    test library: right after the 2nd all-to-all) aborts the exchange: it
+    returns its error, its peer -- blocked in the 3rd all-to-all -- returns
+    ZK_ERR_RCCL instead of hanging, and the aborted exchange refuses further
+    proofs;
+  * a rank passing a witness slice of the wrong length fails on EVERY rank
+    with ZK_ERR_ARG (the status agreement), and the exchange stays usable;
+  * ZK_OPT_DIST_QUOTIENT = 0 (each rank the whole quotient, whole witness)
+    gives the same partial as the distributed quotient;
+  * a non-canonical value in a variable no row references (so no stage reads
+    it) is still rejected by the rank var_owner gives it."""
 import json
 import os
 import socket
@@ -35,7 +42,7 @@ def _free_port():
         return so.getsockname()[1]
 
 
-def _worker(rank, world, port, log_n, seed, out_dir, fault):
+def _worker(rank, world, port, log_n, seed, out_dir, mode):
     import importlib
     import sys
     sys.path.insert(0, ROOT)
@@ -73,9 +80,34 @@ def _worker(rank, world, port, log_n, seed, out_dir, fault):
     dist.all_gather_object(parts, part)
     if rank == 0:
         res["proof"] = [int(w) for w in zkp.Prover.combine(parts, r, s).words]
-    if fault:
+    if mode == "edge":
+        # a short slice on rank 1: ZK_ERR_ARG on both ranks, no hang
+        try:
+            zkp.Prover.prove_partial_host(dpk, zs[:-1] if rank == 1 else zs, len(z), 1, r, s)
+            res["short_slice_error"] = None
+        except Exception as e:   # noqa: BLE001 -- the kind is the result
+            res["short_slice_error"] = type(e).__name__
+        res["after_short_equal"] = zkp.Prover.prove_partial_host(dpk, zs, len(z), 1, r, s) == part
+        # the replicated quotient: whole witness, same partial
+        ctx.set_option(zkp.ZK_OPT_DIST_QUOTIENT, 0)
+        res["replicated_ranges"] = [[int(a), int(b)] for a, b in dpk.witness_ranges()]
+        res["replicated_equal"] = zkp.Prover.prove_partial_host(dpk, dpk.witness_slice(z), len(z), 1, r, s) == part
+        ctx.set_option(zkp.ZK_OPT_DIST_QUOTIENT, -1)
+        # one extra variable that no row references, holding r (non-canonical)
+        csr = zkp.CSRMatrices.synthetic(n)
+        qx = zkp.QAP(zkp.CSRMatrices(n, 3 * n + 2, csr.mats))
+        dx = zkp.CRS.generate_device(ctx, qx, zkp.SetupParams(*params), 1, shard=rank, nshards=world)
+        zx = np.concatenate([z, np.array([zkp.to_limbs(zkp.R)], dtype=np.uint64)])
+        res["extra_in_ranges"] = any(int(a) <= 3 * n + 1 < int(b) for a, b in dx.witness_ranges())
+        try:
+            zkp.Prover.prove_partial_host(dx, dx.witness_slice(zx), len(zx), 1, r, s)
+            res["extra_error"] = None
+        except Exception as e:   # noqa: BLE001
+            res["extra_error"] = type(e).__name__
+        dx.free()
+    if mode == "fault":
         if rank == 1:
-            ctx.set_option(zkp.ZK_OPT_FAULT_AFTER_EXCHANGE, 2)
+            ctx.test_fault_after_exchange(2)
         t = time.perf_counter()
         try:
             zkp.Prover.prove_partial_host(dpk, zs, len(z), 1, r, s)
@@ -96,8 +128,8 @@ def _worker(rank, world, port, log_n, seed, out_dir, fault):
         dist.destroy_process_group()
 
 
-def _run(tmp_path, world, log_n, seed, fault):
-    mp.spawn(_worker, args=(world, _free_port(), log_n, seed, str(tmp_path), fault), nprocs=world, join=True)
+def _run(tmp_path, world, log_n, seed, mode):
+    mp.spawn(_worker, args=(world, _free_port(), log_n, seed, str(tmp_path), mode), nprocs=world, join=True)
     return [json.load(open(tmp_path / f"rank{k}.json")) for k in range(world)]
 
 
@@ -119,7 +151,7 @@ def _oracle_proof(oracle, log_n, seed):
 @pytest.mark.parametrize("world", [2, 4])
 def test_host_exchange_sliced_witness_matches_oracle(oracle, tmp_path, world):
     log_n, seed = 10, 31337 + world
-    res = _run(tmp_path, world, log_n, seed, False)
+    res = _run(tmp_path, world, log_n, seed, "normal")
     assert res[0]["proof"] == _oracle_proof(oracle, log_n, seed)
     for r in res:
         assert r["exchange_max"] == 3 * (world - 1)
@@ -131,10 +163,25 @@ def test_host_exchange_sliced_witness_matches_oracle(oracle, tmp_path, world):
 @pytest.mark.timeout(300)
 def test_rank_failure_mid_quotient_aborts_peers(oracle, tmp_path):
     log_n, seed = 10, 4711
-    res = _run(tmp_path, 2, log_n, seed, True)
+    res = _run(tmp_path, 2, log_n, seed, "fault")
     assert res[0]["proof"] == _oracle_proof(oracle, log_n, seed)
     assert res[1]["fault_error"] == "DeviceError"        # the injected rank-local failure
     assert res[0]["fault_error"] == "ExchangeError"      # the peer: ZK_ERR_RCCL, not a hang
     assert res[0]["fault_s"] < 45 and res[1]["fault_s"] < 45
     for r in res:
         assert r["after_abort_error"] == "ExchangeError"
+
+
+@pytest.mark.timeout(300)
+def test_slice_errors_replicated_quotient_and_unreferenced_variable(oracle, tmp_path):
+    log_n, seed = 10, 2718
+    res = _run(tmp_path, 2, log_n, seed, "edge")
+    assert res[0]["proof"] == _oracle_proof(oracle, log_n, seed)
+    zlen = 3 * (1 << log_n) + 1
+    for r in res:
+        assert r["short_slice_error"] == "ValueError", r      # both ranks, through the agreement
+        assert r["after_short_equal"], r                       # the exchange survived
+        assert r["replicated_ranges"] == [[0, zlen]] and r["replicated_equal"], r
+    # var_owner gives the unreferenced variable (index 3n+1 of 3n+2) to rank 1
+    assert res[1]["extra_in_ranges"] and res[1]["extra_error"] == "ValueError", res[1]
+    assert not res[0]["extra_in_ranges"] and res[0]["extra_error"] is None, res[0]

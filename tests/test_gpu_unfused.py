@@ -61,7 +61,9 @@ def test_three_window_plan_matches_oracle(zkp, oracle, log_n):
 
 def test_options_reject_unknown_values(zkp):
     with zkp.Context(0) as ctx:
-        for opt, val in ((zkp.ZK_OPT_QUOTIENT_PATH, 2), (zkp.ZK_OPT_PROVE_WIN_C, 17), (99, 0)):
+        # 4: the old fault-injection option, now only in libzkp_amd_test.so
+        for opt, val in ((zkp.ZK_OPT_QUOTIENT_PATH, 2), (zkp.ZK_OPT_PROVE_WIN_C, 17), (zkp.ZK_OPT_DIST_QUOTIENT, 1),
+                         (4, 2), (99, 0)):
             with pytest.raises(ValueError):
                 ctx.set_option(opt, val)
         for sched in (1, 4, 9):

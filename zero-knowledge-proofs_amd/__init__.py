@@ -26,6 +26,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # ZK_AMD_LIB: an alternative build of the same library (tooling: A/B runs of
 # variant builds; the library itself reads no environment variables)
 LIB_PATH = os.environ.get("ZK_AMD_LIB") or os.path.join(_HERE, "libzkp_amd.so")
+# the GPU tests' diagnostic hooks (include/zkp_test.h), built on top of
+# libzkp_amd.so; the product path never loads it
+TEST_LIB_PATH = os.path.join(os.path.dirname(LIB_PATH), "libzkp_amd_test.so")
 
 R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001  # Fr modulus
 
@@ -44,14 +47,15 @@ EXPORTS = (
     "zk_groth16_prove", "zk_groth16_prove_dev", "zk_pk_upload_shard",
     "zk_groth16_setup_dev_shard", "zk_groth16_prove_partial", "zk_groth16_prove_combine",
     "zk_proof_serialize_compressed", "zk_rccl_unique_id", "zk_ctx_attach_rccl",
-    "zk_test_prove_virtual_shards", "zk_proof_deserialize_compressed", "zk_groth16_verify",
+    "zk_proof_deserialize_compressed", "zk_groth16_verify",
     "zk_groth16_verify_batch", "zk_pairing_product_is_one", "zk_msm_g1_upload_windows",
     "zk_msm_g2_upload_windows", "zk_build_id", "zk_ctx_set_schedule", "zk_qap_evaluate_at",
     "zk_poly_evaluate_batch", "zk_synthetic_witness_dev", "zk_ctx_set_option", "zk_ctx_timeline_read",
     "zk_ctx_attach_exchange", "zk_groth16_witness_ranges", "zk_groth16_prove_partial_host",
-    "zk_test_exchange",
 )
-ZK_OPT_QUOTIENT_PATH, ZK_OPT_PROVE_WIN_C, ZK_OPT_EXCHANGE_TIMEOUT_MS, ZK_OPT_FAULT_AFTER_EXCHANGE = 1, 2, 3, 4
+# include/zkp_test.h (libzkp_amd_test.so)
+TEST_EXPORTS = ("zk_test_prove_virtual_shards", "zk_test_exchange", "zk_test_fault_after_exchange")
+ZK_OPT_QUOTIENT_PATH, ZK_OPT_PROVE_WIN_C, ZK_OPT_EXCHANGE_TIMEOUT_MS, ZK_OPT_DIST_QUOTIENT = 1, 2, 3, 5
 CSRC = os.path.join(_HERE, "csrc")
 
 
@@ -188,6 +192,24 @@ def lib():
     return _lib
 
 
+_test_lib = None
+
+
+def test_lib():
+    """Load libzkp_amd_test.so (include/zkp_test.h: virtual ranks, the bare
+    exchange, fault injection) on top of libzkp_amd.so -- tests only."""
+    global _test_lib
+    if _test_lib is None:
+        lib()
+        if not os.path.exists(TEST_LIB_PATH):
+            raise ImportError(f"{TEST_LIB_PATH} not built: run `make -C zero-knowledge-proofs_amd/csrc`")
+        T = C.CDLL(TEST_LIB_PATH)
+        for name in TEST_EXPORTS:
+            getattr(T, name).restype = C.c_int
+        _test_lib = T
+    return _test_lib
+
+
 def _p(a):
     return C.c_void_p(a.ctypes.data)
 
@@ -206,8 +228,9 @@ def source_hash():
     for f in names:
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(fh.read())
-    with open(os.path.join(os.path.dirname(_HERE), "include", "zkp.h"), "rb") as fh:
-        h.update(fh.read())
+    for hdr in ("zkp.h", "zkp_test.h"):
+        with open(os.path.join(os.path.dirname(_HERE), "include", hdr), "rb") as fh:
+            h.update(fh.read())
     return h.hexdigest()[:16]
 
 
@@ -297,9 +320,15 @@ class Context:
         attached exchange (RCCL or host-staged); returns the agreed max,
         raises ExchangeError when a received chunk is wrong."""
         out = C.c_int32()
-        _check(lib().zk_test_exchange(C.c_void_p(self._h), C.c_size_t(chunk_bytes), C.c_int32(status),
-                                      C.byref(out)), self, "zk_test_exchange")
+        _check(test_lib().zk_test_exchange(C.c_void_p(self._h), C.c_size_t(chunk_bytes), C.c_int32(status),
+                                           C.byref(out)), self, "zk_test_exchange")
         return out.value
+
+    def test_fault_after_exchange(self, k):
+        """zk_test_fault_after_exchange: the next distributed-quotient proof
+        on this ctx fails right after its k-th all-to-all (tests only)."""
+        _check(test_lib().zk_test_fault_after_exchange(C.c_void_p(self._h), C.c_int(int(k))), self,
+               "zk_test_fault_after_exchange")
 
     def attach_exchange(self, exchange, rank, world):
         """zk_ctx_attach_exchange: the distributed quotient of sharded keys
@@ -338,8 +367,10 @@ class Context:
 
     def set_option(self, option, value):
         """zk_ctx_set_option: ZK_OPT_QUOTIENT_PATH (-1 by size, 0 small-domain,
-        1 large-domain) or ZK_OPT_PROVE_WIN_C (0 by size, 16, 22; keys made
-        afterwards).  Explicit path choices for tests and A/B runs."""
+        1 large-domain), ZK_OPT_PROVE_WIN_C (0 by size, 16, 22; keys made
+        afterwards), ZK_OPT_EXCHANGE_TIMEOUT_MS (>= 1) or ZK_OPT_DIST_QUOTIENT
+        (-1 distributed when an exchange of the key's shape is attached, 0
+        replicated).  Explicit path choices for tests and A/B runs."""
         _check(lib().zk_ctx_set_option(C.c_void_p(self._h), C.c_int(int(option)), C.c_int64(int(value))), self,
                "zk_ctx_set_option")
 
@@ -922,7 +953,7 @@ class Prover:
         ctx = dpks[0].ctx
         arr = (C.c_void_p * len(dpks))(*[C.c_void_p(d._h) for d in dpks])
         out = _Proof()
-        rc = lib().zk_test_prove_virtual_shards(C.c_void_p(ctx._h), arr, C.c_uint32(len(dpks)),
+        rc = test_lib().zk_test_prove_virtual_shards(C.c_void_p(ctx._h), arr, C.c_uint32(len(dpks)),
                                                 C.c_void_p(d_z_ptr), C.c_size_t(zlen), C.c_size_t(num_public),
                                                 C.byref(_fr(r)), C.byref(_fr(s)), C.byref(out))
         _check(rc, ctx, "zk_test_prove_virtual_shards")

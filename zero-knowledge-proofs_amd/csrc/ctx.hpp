@@ -48,6 +48,8 @@ struct zk_ctx {
   int quot_path = -1;                          // -1 by domain size, 0 small-domain, 1 large-domain
   int prove_win_c = 0;                         // 0 by size, else 16 or 22 (keys made after the call)
   double exch_timeout_ms = 60000;              // watchdog of an attached exchange
+  int dist_quotient = -1;                      // -1 distributed when an exchange of the key's shape
+                                               // is attached, 0 never (each rank the whole quotient)
 
   zk::NttDomain& domain(uint32_t log_n);
 };
@@ -85,7 +87,9 @@ bool fr_canonical(const zk_fr& a);
 void check_canonical(const void* d_z, uint64_t n, uint32_t* d_flags, hipStream_t st);
 // the witness ranges of a finished key (its idx vectors and shard) from the
 // host constraint matrices: fills pk.wr_dist
-void pk_witness_ranges(zk_pk_dev& pk, const zk_r1cs_csr* q, hipStream_t st);
+// (own: var_owner of the key's shape; its variables owned by this shard
+// are added, so every z entry is read -- and checked canonical -- by some rank)
+void pk_witness_ranges(zk_pk_dev& pk, const zk_r1cs_csr* q, const std::vector<uint8_t>& own, hipStream_t st);
 // Which shard holds variable v's A / B1 / B2 / IC bases: with a distributed
 // quotient possible (nshards 2, 4 or 8, n % nshards^2 == 0) the shard whose
 // quotient rows first reference v, so a rank's MSM variables are the ones

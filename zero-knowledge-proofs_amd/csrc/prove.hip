@@ -297,7 +297,7 @@ zk_pk_dev* pk_upload(zk_ctx* ctx, const zk_pk* pk, const zk_r1cs_csr* q, uint32_
   }
   // the a/b vectors may be shorter than V (core:171 `i < pk.a_g1.len()`): indices stay < V.
   pk_precompute_windows(ctx, *d);
-  pk_witness_ranges(*d, q, st);
+  pk_witness_ranges(*d, q, own, st);
   return d.release();
 }
 
@@ -325,8 +325,12 @@ std::vector<uint8_t> var_owner(const zk_r1cs_csr* q, uint64_t n, uint32_t N) {
 // z_0 (the constant check, core:89-93), the variables behind its compacted
 // A / B2 / B1 / IC bases (the idx vectors) and the columns of the rows its
 // column slice evaluates (dist.hip stage A: rows a m + rank q + b', a < N,
-// b' < q).  Sorted, merged into ranges.
-void pk_witness_ranges(zk_pk_dev& pk, const zk_r1cs_csr* q, hipStream_t st) {
+// b' < q), plus the variables var_owner gives this shard: a variable no row
+// references and whose bases are all the identity is read by no stage, but
+// it must still be checked canonical by some rank (the one-GPU prove rejects
+// z_i >= r anywhere).  For a variable rows do reference, its owner's rows
+// read it anyway.  Sorted, merged into ranges.
+void pk_witness_ranges(zk_pk_dev& pk, const zk_r1cs_csr* q, const std::vector<uint8_t>& own, hipStream_t st) {
   pk.wr_dist.clear();
   if (pk.nshards < 2 || !dist_quotient_ok(pk.n, (int)pk.nshards)) return;
   std::vector<uint32_t> vars;
@@ -339,6 +343,8 @@ void pk_witness_ranges(zk_pk_dev& pk, const zk_r1cs_csr* q, hipStream_t st) {
   }
   ZK_HIP(hipStreamSynchronize(st));
   vars.push_back(0);
+  for (uint64_t v = 0; v < own.size(); v++)
+    if (own[v] == pk.shard) vars.push_back((uint32_t)v);
   const uint64_t N = pk.nshards, m = pk.n / N, qq = m / N;
   const uint64_t* rps[3] = {q->a_rowptr, q->b_rowptr, q->c_rowptr};
   const uint32_t* cols[3] = {q->a_col, q->b_col, q->c_col};
@@ -483,8 +489,10 @@ static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipS
 // A sharded key whose ctx is attached to the matching exchange (an RCCL
 // communicator, or a host-staged one) computes its quotient distributed
 // (three all-to-alls per proof).
+// zk_ctx_set_option(ZK_OPT_DIST_QUOTIENT, 0) turns it off: every rank then
+// computes the whole quotient (bench.py's replicated-quotient comparison).
 static bool uses_dist_quotient(const zk_ctx* ctx, const zk_pk_dev* pk) {
-  return pk->nshards > 1 && ctx->exch && ctx->exch->world == (int)pk->nshards &&
+  return ctx->dist_quotient != 0 && pk->nshards > 1 && ctx->exch && ctx->exch->world == (int)pk->nshards &&
          ctx->exch->rank == (int)pk->shard && dist_quotient_ok(pk->n, (int)pk->nshards);
 }
 
@@ -607,6 +615,10 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   // 0.37 ms slower: profiles/r03_ab_quotient_first_rejected.txt)
   launch_msms();
   run_quotient();
+  // the exchange watchdog below counts from here: a host-staged exchange has
+  // finished its all-to-alls inside run_quotient, and only local GPU work
+  // (RCCL: the enqueued collectives) is left
+  const auto t_quot = clk::now();
   ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
   {
     const int h_slot[1] = {MSM_H};
@@ -630,7 +642,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   for (int left = 3; left > 0;) {
     // the H MSM waits for the peers' quotient stages: a dead peer must end
     // this proof (ZK_ERR_RCCL, the exchange aborted) instead of hanging it
-    if (dist && (ctx->exch->async_error() || ms_since(t_start) > ctx->exch->timeout_ms))
+    if (dist && (ctx->exch->async_error() || ms_since(t_quot) > ctx->exch->timeout_ms))
       throw Error(ZK_ERR_RCCL, "distributed quotient: a peer did not answer within the exchange timeout");
     bool progressed = false;
     for (int wi = 0; wi < 3; wi++) {
@@ -718,13 +730,17 @@ int prove_impl(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, size_t zlen, s
 
 // z_host / ranges: a host witness slice (zk_groth16_prove_partial_host) to
 // upload first, after the ranks agreed, instead of the device witness d_z.
+// bad_slice: the host slice does not match the ranges (ZK_ERR_ARG) -- with a
+// distributed quotient it goes into the status agreement like every other
+// input error, so the peers return with this rank instead of waiting in the
+// first all-to-all.
 static int prove_partial_common(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, const zk_fr* z_host,
                                 const std::vector<uint64_t>* ranges, size_t zlen, size_t num_public,
-                                const zk_fr* r, const zk_fr* s, zk_prove_partial* out) {
+                                const zk_fr* r, const zk_fr* s, zk_prove_partial* out, bool bad_slice = false) {
   std::memset(out, 0, sizeof *out);
   Partial p{};
   int local = ZK_OK;
-  if (!fr_canonical(*r) || !fr_canonical(*s)) local = ZK_ERR_ARG;
+  if (bad_slice || !fr_canonical(*r) || !fr_canonical(*s)) local = ZK_ERR_ARG;
   else if (num_public >= zlen || zlen != pk->V) local = ZK_ERR_INVALID_WITNESS;
   const bool dist = uses_dist_quotient(ctx, pk);
   if (dist && ctx->exch->broken) {
@@ -805,13 +821,11 @@ int prove_partial_host_impl(zk_ctx* ctx, const zk_pk_dev* pk, const zk_fr* z_sli
   const std::vector<uint64_t> ranges = witness_ranges(ctx, pk);
   size_t want = 0;
   for (size_t k = 0; k + 1 < ranges.size(); k += 2) want += ranges[k + 1] - ranges[k];
-  if (slice_len != want || (want && !z_slice)) {
-    std::memset(out, 0, sizeof *out);
+  const bool bad = slice_len != want || (want && !z_slice);
+  if (bad)
     ctx->err = "witness slice length " + std::to_string(slice_len) + " != " + std::to_string(want) +
                " (zk_groth16_witness_ranges)";
-    return ZK_ERR_ARG;
-  }
-  return prove_partial_common(ctx, pk, nullptr, z_slice, &ranges, zlen, num_public, r, s, out);
+  return prove_partial_common(ctx, pk, nullptr, z_slice, &ranges, zlen, num_public, r, s, out, bad);
 }
 
 // N virtual ranks of a sharded key on ONE device: the distributed quotient's

@@ -244,6 +244,22 @@ def setup(csr, params, num_public, nthreads=1):
     return rc, pk, vk
 
 
+def setup_sample(csr, params, num_public, vars, hidx):
+    """Sampled key entries by or_setup's arithmetic: {a_g1, b_g1, b_g2, ic}
+    for the variables in vars (ic: pk ic_g1[v - num_public - 1] for v >
+    num_public) and h_g1 for the coefficient indices in hidx."""
+    vars = np.ascontiguousarray(vars, dtype=np.uint64)
+    hidx = np.ascontiguousarray(hidx, dtype=np.uint64)
+    out = {"a_g1": np.zeros((len(vars), 13), dtype=np.uint64), "b_g1": np.zeros((len(vars), 13), dtype=np.uint64),
+           "b_g2": np.zeros((len(vars), 25), dtype=np.uint64), "ic": np.zeros((len(vars), 13), dtype=np.uint64),
+           "h_g1": np.zeros((len(hidx), 13), dtype=np.uint64)}
+    par = np.array([int_to_limbs(p, 4) for p in params], dtype=np.uint64).reshape(-1)
+    rc = lib().or_setup_sample(C.byref(csr.s), _p(par), C.c_uint64(num_public), _p(vars), C.c_uint64(len(vars)),
+                               _p(hidx), C.c_uint64(len(hidx)), _p(out["a_g1"]), _p(out["b_g1"]),
+                               _p(out["b_g2"]), _p(out["ic"]), _p(out["h_g1"]))
+    return rc, out
+
+
 def prove(pk, csr, z, num_public, r, s):
     """Returns (rc, proof words[51])."""
     proof = np.zeros(51, dtype=np.uint64)

@@ -774,6 +774,55 @@ int or_setup(const or_r1cs *cs, const u64 params[20], u64 num_public, or_pk *pk,
   return OR_OK;
 }
 
+/* Sampled entries of the same key, for checking a setup too large to
+ * restate whole (the sharded 2^24 GPU setup): the base of each listed
+ * variable v in a_g1 / b_g1 / b_g2 (setup:185-207) and ic (setup:210-229:
+ * pk ic_g1[v - num_public - 1] for v > num_public, the vk's ic_g1[v]
+ * otherwise), and of each listed coefficient index i < n in h_g1
+ * (setup:232-241), by exactly or_setup's arithmetic: A_i(tau~) etc. from the
+ * whole sparse Lagrange pass, lo64 scalars, fixed-base multiples.  Outputs
+ * 13 (G1) / 25 (G2) words per sample; NULL outputs are skipped. */
+int or_setup_sample(const or_r1cs *cs, const u64 params[20], u64 num_public, const u64 *vars, u64 nv,
+                    const u64 *hidx, u64 nh, u64 *a_g1, u64 *b_g1, u64 *b_g2, u64 *ic_g1, u64 *h_g1) {
+  u64 V = cs->num_variables, n = or_domain_size(cs->num_constraints);
+  fr P[5];
+  for (int i = 0; i < 5; i++) fr_to_mont(&P[i], params + 4 * i);
+  for (int i = 0; i < 4; i++) if (fr_is_zero(&P[i])) return OR_ERR_SETUP_PARAMS;
+  if (num_public >= V) return OR_ERR_SETUP_PARAMS;
+  for (u64 k = 0; k < nv; k++) if (vars[k] >= V) return OR_ERR_SETUP_PARAMS;
+  for (u64 k = 0; k < nh; k++) if (hidx[k] >= n) return OR_ERR_SETUP_PARAMS;
+  fr al, be, ga, de, ta;
+  lo64_fr(&al, &P[0]); lo64_fr(&be, &P[1]); lo64_fr(&ga, &P[2]); lo64_fr(&de, &P[3]); lo64_fr(&ta, &P[4]);
+  if (fr_is_zero(&de) || fr_is_zero(&ga)) return OR_ERR_SETUP_PARAMS;
+  fr *av = (fr *)malloc(sizeof(fr) * V), *bv = (fr *)malloc(sizeof(fr) * V), *cv = (fr *)malloc(sizeof(fr) * V);
+  qap_eval_mont(cs, &ta, av, bv, cv);
+  g1_jac g1; g1_from_aff(&g1, &G1_GEN);
+  g2_jac g2; g2_from_aff(&g2, &G2_GEN);
+  g1_aff *t1 = (g1_aff *)malloc(sizeof(g1_aff) * 2048);
+  g2_aff *t2 = (g2_aff *)malloc(sizeof(g2_aff) * 2048);
+  g1_fb_table(t1, &g1); g2_fb_table(t2, &g2);
+  fr dinv, ginv; fr_inv(&dinv, &de); fr_inv(&ginv, &ga);
+  for (u64 k = 0; k < nv; k++) {
+    const u64 v = vars[k];
+    g1_jac j; g1_aff a; g2_jac j2; g2_aff a2;
+    if (a_g1) { g1_fb_mul(&j, t1, fr_lo64(&av[v])); g1_to_aff(&a, &j); g1_store(a_g1 + 13 * k, &a); }
+    if (b_g1) { g1_fb_mul(&j, t1, fr_lo64(&bv[v])); g1_to_aff(&a, &j); g1_store(b_g1 + 13 * k, &a); }
+    if (b_g2) { g2_fb_mul(&j2, t2, fr_lo64(&bv[v])); g2_to_aff(&a2, &j2); g2_store(b_g2 + 25 * k, &a2); }
+    if (ic_g1) {
+      fr t, u; fr_mul(&t, &be, &av[v]); fr_mul(&u, &al, &bv[v]); fr_add(&t, &t, &u); fr_add(&t, &t, &cv[v]);
+      fr_mul(&t, &t, v > num_public ? &dinv : &ginv);
+      g1_fb_mul(&j, t1, fr_lo64(&t)); g1_to_aff(&a, &j); g1_store(ic_g1 + 13 * k, &a);
+    }
+  }
+  for (u64 k = 0; k < nh && h_g1; k++) {
+    u64 e[4] = {hidx[k], 0, 0, 0};
+    fr tp, t; fr_pow(&tp, &ta, e, 1); fr_mul(&t, &tp, &dinv);
+    g1_jac j; g1_aff a; g1_fb_mul(&j, t1, fr_lo64(&t)); g1_to_aff(&a, &j); g1_store(h_g1 + 13 * k, &a);
+  }
+  free(av); free(bv); free(cv); free(t1); free(t2);
+  return OR_OK;
+}
+
 /* ------------------------------------------------------------------------ */
 /* prove: Prover::prove (crates/groth16-core/src/lib.rs:139-272)            */
 /* ------------------------------------------------------------------------ */

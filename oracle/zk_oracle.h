@@ -140,6 +140,12 @@ void or_qap_eval_at(const or_r1cs *cs, const uint64_t t[4], uint64_t *a_vals,
 /* params = alpha,beta,gamma,delta,tau (5 x 4 limbs, canonical). */
 int or_setup(const or_r1cs *cs, const uint64_t params[20], uint64_t num_public,
              or_pk *pk, or_vk *vk, int nthreads);
+/* Sampled key entries by or_setup's arithmetic: bases of variables vars[k]
+ * in a_g1 / b_g1 / b_g2 / ic (pk ic for v > num_public, else vk ic) and of
+ * coefficients hidx[k] in h_g1; NULL outputs skipped. */
+int or_setup_sample(const or_r1cs *cs, const uint64_t params[20], uint64_t num_public,
+                    const uint64_t *vars, uint64_t nv, const uint64_t *hidx, uint64_t nh,
+                    uint64_t *a_g1, uint64_t *b_g1, uint64_t *b_g2, uint64_t *ic_g1, uint64_t *h_g1);
 /* proof = a (13) | b (25) | c (13) words */
 int or_prove(const or_pk *pk, const or_r1cs *cs, const uint64_t *z, uint64_t zlen,
              uint64_t num_public, const uint64_t r[4], const uint64_t s[4],

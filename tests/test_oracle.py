@@ -185,3 +185,27 @@ def test_oracle_threads_do_not_change_results(oracle, pyref):
                 assert np.array_equal(bases[i], p)
     finally:
         oracle.set_threads(saved)
+
+
+def test_setup_sample_equals_full_setup(oracle):
+    """or_setup_sample (sampled key entries, used to check the sharded 2^24
+    GPU setup) gives exactly or_setup's entries."""
+    import numpy as np
+    import pyref
+    n = 1 << 8
+    csr = oracle.CSR.synthetic(n)
+    rng = pyref.SplitMix64(99)
+    params = [rng.fr() for _ in range(5)]
+    rc, pk, vk = oracle.setup(csr, params, 1, nthreads=4)
+    assert rc == 0
+    vars_ = np.array([0, 1, 2, 3, 5, 100, 3 * n], dtype=np.uint64)
+    hidx = np.array([0, 1, 7, n - 1], dtype=np.uint64)
+    rc, smp = oracle.setup_sample(csr, params, 1, vars_, hidx)
+    assert rc == 0
+    assert np.array_equal(smp["a_g1"], pk.a_g1[vars_])
+    assert np.array_equal(smp["b_g1"], pk.b_g1[vars_])
+    assert np.array_equal(smp["b_g2"], pk.b_g2[vars_])
+    assert np.array_equal(smp["h_g1"], pk.h_g1[hidx])
+    for k, v in enumerate(vars_):
+        want = pk.ic_g1[v - 2] if v > 1 else vk.ic_g1[v]
+        assert np.array_equal(smp["ic"][k], want), v

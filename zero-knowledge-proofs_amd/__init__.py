@@ -54,7 +54,8 @@ EXPORTS = (
     "zk_ctx_attach_exchange", "zk_groth16_witness_ranges", "zk_groth16_prove_partial_host",
 )
 # include/zkp_test.h (libzkp_amd_test.so)
-TEST_EXPORTS = ("zk_test_prove_virtual_shards", "zk_test_exchange", "zk_test_fault_after_exchange")
+TEST_EXPORTS = ("zk_test_prove_virtual_shards", "zk_test_exchange", "zk_test_fault_after_exchange",
+                "zk_test_pk_bases", "zk_test_pk_info")
 ZK_OPT_QUOTIENT_PATH, ZK_OPT_PROVE_WIN_C, ZK_OPT_EXCHANGE_TIMEOUT_MS, ZK_OPT_DIST_QUOTIENT = 1, 2, 3, 5
 CSRC = os.path.join(_HERE, "csrc")
 
@@ -751,6 +752,29 @@ class DeviceProvingKey:
         _check(lib().zk_groth16_witness_ranges(C.c_void_p(self.ctx._h), C.c_void_p(self._h), _p(out),
                                                C.c_size_t(n.value), C.byref(n)), self.ctx, "zk_groth16_witness_ranges")
         return out[:n.value]
+
+    def test_info(self):
+        """zk_test_pk_info (test library): (win, win_c, shard, nshards)."""
+        v = [C.c_uint32() for _ in range(4)]
+        _check(test_lib().zk_test_pk_info(C.c_void_p(self._h), *[C.byref(x) for x in v]), None, "zk_test_pk_info")
+        return tuple(x.value for x in v)
+
+    def test_bases(self, slot, window=0):
+        """zk_test_pk_bases (test library): (variable / coefficient index per
+        compacted base, canonical words of the compacted bases + extras,
+        number of extras) of one MSM slot's window copy."""
+        cnt, nex = C.c_size_t(), C.c_size_t()
+        _check(test_lib().zk_test_pk_bases(C.c_void_p(self.ctx._h), C.c_void_p(self._h), C.c_int(slot),
+                                           C.c_int(window), None, None, C.c_size_t(0), C.byref(cnt), C.byref(nex)),
+               self.ctx, "zk_test_pk_bases")
+        tot = cnt.value + nex.value
+        words = G2_WORDS if slot == 1 else G1_WORDS
+        idx = np.zeros(max(cnt.value, 1), dtype=np.uint32)
+        out = np.zeros((max(tot, 1), words), dtype=np.uint64)
+        _check(test_lib().zk_test_pk_bases(C.c_void_p(self.ctx._h), C.c_void_p(self._h), C.c_int(slot),
+                                           C.c_int(window), _p(idx), _p(out), C.c_size_t(max(tot, 1)),
+                                           C.byref(cnt), C.byref(nex)), self.ctx, "zk_test_pk_bases")
+        return idx[:cnt.value], out[:tot], nex.value
 
     def witness_slice(self, assignment):
         """This shard's part of a full witness (rows of every witness range, in order)."""

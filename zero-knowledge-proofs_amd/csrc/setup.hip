@@ -278,6 +278,22 @@ static void to_abi(const typename C::A* d_in, size_t n, void* host_out, hipStrea
   ZK_HIP(hipStreamSynchronize(st));
 }
 
+// n device affine points (Montgomery) `stride` bytes apart (0 = packed) ->
+// canonical ABI words in host memory (the test library's key readback)
+void bases_to_abi_host(bool g2, const void* d_in, uint32_t stride, size_t n, uint64_t* host_out, hipStream_t st) {
+  if (!n) return;
+  const size_t asz = g2 ? sizeof(G2A) : sizeof(G1A);
+  DevBuf packed;
+  const void* src = d_in;
+  if (stride && stride != asz) {
+    packed.ensure(asz * n);
+    ZK_HIP(hipMemcpy2DAsync(packed.p, asz, d_in, stride, asz, n, hipMemcpyDeviceToDevice, st));
+    src = packed.p;
+  }
+  if (g2) to_abi<G2>(static_cast<const G2A*>(src), n, host_out, st);
+  else to_abi<G1>(static_cast<const G1A*>(src), n, host_out, st);
+}
+
 // host-side generator multiple by a full-width canonical scalar -> ABI
 template <class C, class HX>
 static void gen_mul_abi(const HX& G, const zk_fr& k, void* out) {

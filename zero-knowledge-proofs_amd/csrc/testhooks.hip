@@ -9,6 +9,7 @@
 #include "../../include/zkp_test.h"
 
 namespace zk {
+void bases_to_abi_host(bool g2, const void* d_in, uint32_t stride, size_t n, uint64_t* host_out, hipStream_t st);
 int prove_virtual_shards_impl(zk_ctx*, const zk_pk_dev* const*, uint32_t, const void*, size_t, size_t,
                               const zk_fr*, const zk_fr*, zk_proof*);
 }  // namespace zk
@@ -61,5 +62,35 @@ int zk_test_exchange(zk_ctx* ctx, size_t chunk_bytes, int32_t status, int32_t* o
 int zk_test_fault_after_exchange(zk_ctx* ctx, int k) {
   if (!ctx || k < 0 || k > 3 || !ctx->exch) return ZK_ERR_ARG;
   ctx->exch->fault_after = k;
+  return ZK_OK;
+}
+
+int zk_test_pk_bases(zk_ctx* ctx, const zk_pk_dev* pk, int slot, int window, uint32_t* idx_out, uint64_t* words_out,
+                     size_t cap, size_t* count, size_t* nextras) {
+  if (!ctx || !pk || !count || !nextras || slot < 0 || slot >= NUM_MSM || window < 0 || window >= pk->win)
+    return ZK_ERR_ARG;
+  const size_t cnt = pk->count[slot], nex = pk->extras[slot], tot = cnt + nex;
+  *count = cnt;
+  *nextras = nex;
+  if (!cap) return ZK_OK;
+  if (cap < tot || !idx_out || !words_out) return ZK_ERR_ARG;
+  ZK_TGUARD(ctx, {
+    const bool g2 = slot == MSM_B2;
+    const size_t asz = g2 ? sizeof(G2A) : sizeof(G1A);
+    const size_t step = pk->stride[slot] ? pk->stride[slot] : asz;
+    const char* base = static_cast<const char*>(pk->bases[slot].p) + (size_t)window * tot * step;
+    if (cnt) ZK_HIP(hipMemcpyAsync(idx_out, pk->idx[slot].p, sizeof(uint32_t) * cnt, hipMemcpyDeviceToHost, ctx->stream));
+    bases_to_abi_host(g2, base, pk->stride[slot], tot, words_out, ctx->stream);
+    ZK_HIP(hipStreamSynchronize(ctx->stream));
+    return ZK_OK;
+  })
+}
+
+int zk_test_pk_info(const zk_pk_dev* pk, uint32_t* win, uint32_t* win_c, uint32_t* shard, uint32_t* nshards) {
+  if (!pk || !win || !win_c || !shard || !nshards) return ZK_ERR_ARG;
+  *win = (uint32_t)pk->win;
+  *win_c = (uint32_t)pk->win_c;
+  *shard = pk->shard;
+  *nshards = pk->nshards;
   return ZK_OK;
 }

@@ -121,6 +121,16 @@ def test_prove_rejects_non_canonical(ctx, zkp, oracle):
         zkp.Prover.prove_device(dpk, dz.data_ptr(), len(zb), 1, 3, 4)
     import ctypes as C
     out = zkp._Proof()
+    r_ok, s_ok = zkp._fr(3), zkp._fr(4)
+    # the host-witness path checks each uploaded part: a bad entry in the
+    # first half (7) and in the second (3n)
+    for bad in (7, 3 * n):
+        zh = z.copy()
+        zh[bad] = _rows_r()
+        zh[bad, 0] += 5
+        rc = zkp.lib().zk_groth16_prove(C.c_void_p(ctx._h), C.c_void_p(dpk._h), zkp._p(zh), C.c_size_t(len(zh)),
+                                        C.c_size_t(1), C.byref(r_ok), C.byref(s_ok), C.byref(out))
+        assert rc == zkp.ZK_ERR_ARG, bad
     for rr, ss in ((R, 4), (3, R + 1)):
         r_fr, s_fr = zkp._Fr(), zkp._Fr()
         for i, x in enumerate(zkp.to_limbs(rr)):
@@ -193,6 +203,10 @@ def test_schedules_give_the_same_proof(ctx, zkp, oracle, log_n):
             p = zkp.Prover.prove_device(dpk, z.data_ptr(), len(zh), 1, r, s)
             torch.cuda.synchronize()
             assert np.array_equal(p.words, oproof), sched
+            # the host-witness prove: z uploaded in two parts, the first
+            # part's MSMs overlapping the second part's copy
+            ph = zkp.Prover.prove(dpk, zkp.Witness(zh, 1), r=r, s=s)
+            assert np.array_equal(ph.words, oproof), ("host", sched)
     finally:
         ctx.set_schedule(-1)
         dpk.free()

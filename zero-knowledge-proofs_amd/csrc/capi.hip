@@ -7,7 +7,8 @@
 
 namespace zk {
 zk_pk_dev* pk_upload(zk_ctx* ctx, const zk_pk* pk, const zk_r1cs_csr* q, uint32_t shard, uint32_t nshards);
-int prove_impl(zk_ctx*, const zk_pk_dev*, const void*, size_t, size_t, const zk_fr*, const zk_fr*, zk_proof*);
+int prove_impl(zk_ctx*, const zk_pk_dev*, const void*, size_t, size_t, const zk_fr*, const zk_fr*, zk_proof*,
+               const zk_fr* z_host = nullptr);
 int prove_partial_impl(zk_ctx*, const zk_pk_dev*, const void*, size_t, size_t, const zk_fr*, const zk_fr*,
                        zk_prove_partial*);
 int prove_partial_host_impl(zk_ctx*, const zk_pk_dev*, const zk_fr*, size_t, size_t, size_t, const zk_fr*,
@@ -53,7 +54,7 @@ zk_ctx* zk_ctx_create(int device) {
     ZK_HIP(hipSetDevice(device));
     std::unique_ptr<zk_ctx> c(new zk_ctx());
     c->device = device;
-    for (int i = 0; i < NUM_MSM; i++) c->msm[i].prof = &c->prof;
+    for (int i = 0; i < NUM_MSM; i++) c->msm[i].prof = c->msm2[i].prof = &c->prof;
     int lo_prio = 0, hi_prio = 0;
     ZK_HIP(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
     ZK_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio));   // quotient + H
@@ -481,10 +482,11 @@ int zk_groth16_prove(zk_ctx* ctx, const zk_pk_dev* pk, const zk_fr* z, size_t zl
                      const zk_fr* r, const zk_fr* s, zk_proof* out) {
   if (!ctx || !pk || !z || !r || !s || !out) return ZK_ERR_ARG;
   ZK_GUARD(ctx, {
+    // the witness crosses PCIe in two parts inside the prove, the first
+    // part's MSMs overlapping the second part's copy (prove.hip)
     ctx->z_canon.ensure(sizeof(zk_fr) * std::max<size_t>(zlen, 1));
-    if (zlen)
-      ZK_HIP(hipMemcpyAsync(ctx->z_canon.p, z, sizeof(zk_fr) * zlen, hipMemcpyHostToDevice, ctx->stream));
-    return prove_impl(ctx, pk, ctx->z_canon.p, zlen, num_public, r, s, out);
+    if (zlen != pk->V) return prove_impl(ctx, pk, ctx->z_canon.p, zlen, num_public, r, s, out);   // the length error
+    return prove_impl(ctx, pk, ctx->z_canon.p, zlen, num_public, r, s, out, z);
   })
 }
 

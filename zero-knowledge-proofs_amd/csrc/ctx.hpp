@@ -33,6 +33,7 @@ struct zk_ctx {
   hipEvent_t ev_done[zk::NUM_MSM] = {};         // per-MSM completion (results downloaded)
   std::string err;
   zk::MsmWork msm[zk::NUM_MSM];
+  zk::MsmWork msm2[zk::NUM_MSM];                // first parts of MSMs split over a host witness upload
   std::map<uint32_t, std::unique_ptr<zk::NttDomain>> domains;
   // prove scratch
   zk::DevBuf z_canon, qabc, flags;   // qabc: the quotient's A, B, C vectors back to back (3n)
@@ -75,6 +76,12 @@ struct zk_pk_dev {
   // [lo, hi) pairs: the z entries this shard reads with a distributed
   // quotient (zk_groth16_witness_ranges); without one it reads all of z
   std::vector<uint64_t> wr_dist;
+  // Host-witness prove (zk_groth16_prove): z crosses PCIe in two parts,
+  // variables [0, vh) then [vh, V); cut[slot] = compacted bases whose
+  // variable is < vh, so the first part's MSMs start while the second part
+  // is still in flight (pk_part_cuts).
+  uint64_t vh = 0;
+  uint32_t cut[zk::NUM_MSM] = {};
 };
 
 namespace zk {
@@ -85,6 +92,8 @@ void pk_precompute_windows(zk_ctx* ctx, zk_pk_dev& pk);
 // flags |= 8 when some of the n canonical Fr at d_z is >= r
 bool fr_canonical(const zk_fr& a);
 void check_canonical(const void* d_z, uint64_t n, uint32_t* d_flags, hipStream_t st);
+// vh and cut[] of a finished key (device binary search over its idx vectors)
+void pk_part_cuts(zk_pk_dev& pk, hipStream_t st);
 // the witness ranges of a finished key (its idx vectors and shard) from the
 // host constraint matrices: fills pk.wr_dist
 // (own: var_owner of the key's shape; its variables owned by this shard

@@ -133,10 +133,12 @@ constexpr uint32_t MSM_DUMMY = 0x7fffffffu;   // entry that contributes nothing
 // every bucket, so off[G] still counts the non-zero digits.
 // Batches call it once per MSM with that MSM's n, its first bucket key_base
 // and key / ent advanced to its first entry.
+// wstride / ioff (shared plans): the segment's point i is base ioff + i of
+// a window-shifted vector whose windows are wstride points apart.
 template <int SW>
 __global__ void __launch_bounds__(256) k_msm_keys(const uint64_t* __restrict__ sc, MsmPlan p, uint32_t n,
-                                                  uint32_t key_base, uint32_t* __restrict__ key,
-                                                  uint32_t* __restrict__ ent) {
+                                                  uint32_t key_base, uint32_t wstride, uint32_t ioff,
+                                                  uint32_t* __restrict__ key, uint32_t* __restrict__ ent) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint64_t s[SW];
@@ -164,7 +166,8 @@ __global__ void __launch_bounds__(256) k_msm_keys(const uint64_t* __restrict__ s
       // for one) -- a zero digit becomes a dummy entry of the MSM's bucket 0
       // that adds nothing
       key[o] = key_base + (mag ? mag - 1 : 0u);
-      ent[o] = mag ? ((uint32_t)o | (neg ? 0x80000000u : 0u)) : MSM_DUMMY;   // base 2^(c w) P_i at w n + i
+      const uint32_t b = (uint32_t)w * wstride + ioff + i;   // base 2^(c w) P_i
+      ent[o] = mag ? (b | (neg ? 0x80000000u : 0u)) : MSM_DUMMY;
     } else {
       key[o] = mag ? p.boff[w] + mag - 1 : p.G;
       ent[o] = i | (neg ? 0x80000000u : 0u);
@@ -586,7 +589,7 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_rowcol(MsmPlan p, co
     X o;
     if (it < niter) {
       const uint32_t t = it * 64 + lane, g = g0 + t * stride;
-      if (t < len && off[g + 1] != off[g]) o = ld_vec(&buckets[g]);
+      if (t < len && (p.all_valid || off[g + 1] != off[g])) o = ld_vec(&buckets[g]);
       else xyzz_set_inf(o);
     } else {
       o = shfl_xor_point(v, 1 << (it - niter));
@@ -685,7 +688,7 @@ __global__ void __launch_bounds__(64 * RW) k_msm_rowcol_q(MsmPlan p, const uint3
     bool have = false;
     if (it < niter) {
       const uint32_t t = it * NQ + j, g = g0 + t * stride;
-      have = t < len && off[g + 1] != off[g];
+      have = t < len && (p.all_valid || off[g + 1] != off[g]);
       if (have) term = ld_vec(&buckets[g]);
     }
     const X o = quad_sum_step<X, RW>(v, it, niter, xs, have, term);
@@ -749,7 +752,7 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_rowcol_pair(MsmPlan 
     XYZZ<Fq2h> o;
     if (it < niter) {
       const uint32_t t = it * 32 + pr, g = g0 + t * stride;
-      if (t < len && off[g + 1] != off[g]) o = ld_pair(&buckets[g]);
+      if (t < len && (p.all_valid || off[g + 1] != off[g])) o = ld_pair(&buckets[g]);
       else xyzz_set_inf(o);
     } else {
       o = shfl_xor_point(v, 2 << (it - niter));
@@ -777,6 +780,38 @@ __global__ void __launch_bounds__(128) k_msm_fixup_pair(const uint32_t* __restri
 #pragma unroll 1
   for (uint32_t t = t0 + 1; t <= t1; t++) acc = tail_add(acc, ld_pair(&partials[2 * (size_t)t]));
   st_pair(&buckets[g], acc);
+}
+
+// Two parts of one split MSM (msm_batch_back COMBINE): bucket g = this
+// part's bucket + the earlier part's, each only where its part had entries,
+// written for EVERY bucket (infinity where both are empty), so the reduction
+// reads them all (MsmPlan::all_valid).
+template <class C>
+__global__ void __launch_bounds__(128) k_msm_combine(const uint32_t* __restrict__ off,
+                                                     const uint32_t* __restrict__ off_prev, uint32_t G,
+                                                     typename C::X* __restrict__ buckets,
+                                                     const typename C::X* __restrict__ prev) {
+  using X = typename C::X;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  X a, b;
+  if (off[g + 1] != off[g]) a = ld_vec(&buckets[g]);
+  else xyzz_set_inf(a);
+  if (off_prev[g + 1] != off_prev[g]) b = ld_vec(&prev[g]);
+  else xyzz_set_inf(b);
+  st_vec(&buckets[g], tail_add(a, b));
+}
+__global__ void __launch_bounds__(128) k_msm_combine_pair(const uint32_t* __restrict__ off,
+                                                          const uint32_t* __restrict__ off_prev, uint32_t G,
+                                                          G2X* __restrict__ buckets, const G2X* __restrict__ prev) {
+  const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
+  if (g >= G) return;   // pair-uniform
+  XYZZ<Fq2h> a, b;
+  if (off[g + 1] != off[g]) a = ld_pair(&buckets[g]);
+  else xyzz_set_inf(a);
+  if (off_prev[g + 1] != off_prev[g]) b = ld_pair(&prev[g]);
+  else xyzz_set_inf(b);
+  st_pair(&buckets[g], tail_add(a, b));
 }
 
 // ------------------------------------------------------------ driver -----
@@ -876,7 +911,7 @@ constexpr uint32_t MSM_FIX_MAX = 8;
 // One MSM (nseg = 1) or a batch of MSMs sharing every phase: segment k's
 // keys start at bucket k << segshift and its entries at sum_{j<k} nwin n_j.
 template <class C>
-static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hipStream_t st) {
+static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hipStream_t st) {
   using X = typename C::X;
   constexpr bool g2 = std::is_same<C, G2>::value;
   MsmPlan& p = w.plan;
@@ -895,6 +930,7 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
   // row/column sums: G2 on lane pairs, G1 on lane quads when there are few
   // (ROWCOL_QUAD_MAX, unsplit), else one lane per add, split to fill the chip
   const bool quad_rc = !g2 && p.nrc <= ROWCOL_QUAD_MAX;
+  p.quad_rc = quad_rc;
   if (!quad_rc && (g2 ? ZK_SPLIT_G2 : ZK_SPLIT_G1)) msm_split_sums(p, rowcol_waves<C>(), g2 ? 32u : 64u);
   w.partials.ensure(sizeof(X) * 2 * (size_t)p.T);
   w.partials2.ensure(sizeof(X) * ((size_t)p.T / 2 + 2));
@@ -925,10 +961,13 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
     if (!nk) continue;
     const uint32_t nb = ceil_div(nk, 256);
     const uint32_t kbase = p.shared ? (uint32_t)k << (p.segshift & 31) : 0u;
+    const uint32_t wstride = segs[k].wstride ? segs[k].wstride : nk;
     uint32_t* ki = w.key_in.as<uint32_t>() + eoff;
     uint32_t* ei = w.ent_in.as<uint32_t>() + eoff;
-    if (sw == 1) k_msm_keys<1><<<nb, 256, 0, st>>>(segs[k].scalars, p, nk, nseg > 1 ? kbase : 0u, ki, ei);
-    else k_msm_keys<4><<<nb, 256, 0, st>>>(segs[k].scalars, p, nk, 0u, ki, ei);
+    if (sw == 1)
+      k_msm_keys<1><<<nb, 256, 0, st>>>(segs[k].scalars, p, nk, nseg > 1 ? kbase : 0u, wstride, segs[k].ioff, ki, ei);
+    else
+      k_msm_keys<4><<<nb, 256, 0, st>>>(segs[k].scalars, p, nk, 0u, nk, 0u, ki, ei);
     ZK_LAUNCH_CHECK();
     eoff += (size_t)nk * p.nwin;
   }
@@ -954,7 +993,18 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
     ZK_LAUNCH_CHECK();
     if (pf) pf->end(st, ph);
   }
-  ph = pf ? pf->begin(st, (w.tag + "msm_merge").c_str(), p.G) : -1;   // buckets split across chunks
+}
+
+template <class C>
+static void msm_back_impl(MsmWork& w, hipStream_t st, int mode, const MsmWork* prev) {
+  using X = typename C::X;
+  constexpr bool g2 = std::is_same<C, G2>::value;
+  MsmPlan& p = w.plan;
+  Prof* pf = w.prof;
+  const uint32_t n = p.n;
+  (void)n;
+  const bool quad_rc = p.quad_rc != 0;
+  int ph = pf ? pf->begin(st, (w.tag + "msm_merge").c_str(), p.G) : -1;   // buckets split across chunks
   w.nbig.ensure(sizeof(uint32_t));
   ZK_HIP(hipMemsetAsync(w.nbig.p, 0, sizeof(uint32_t), st));
   if constexpr (g2)
@@ -985,7 +1035,21 @@ static void msm_launch_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hi
       std::swap(a, b);
     }
   }
+  p.all_valid = 0;
+  if (mode == MSM_BACK_COMBINE) {
+    if (!prev || prev->plan.G != p.G || prev->plan.nseg != p.nseg) throw Error(ZK_ERR_ARG, "msm: combine plans differ");
+    if constexpr (g2)
+      k_msm_combine_pair<<<ceil_div(2 * (size_t)p.G, 128), 128, 0, st>>>(
+          w.off.as<uint32_t>(), prev->off.as<uint32_t>(), p.G, reinterpret_cast<G2X*>(w.buckets.p),
+          reinterpret_cast<const G2X*>(prev->buckets.p));
+    else
+      k_msm_combine<C><<<ceil_div(p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), prev->off.as<uint32_t>(), p.G,
+                                                            w.buckets.as<X>(), prev->buckets.as<X>());
+    ZK_LAUNCH_CHECK();
+    p.all_valid = 1;
+  }
   if (pf) pf->end(st, ph);
+  if (mode == MSM_BACK_FIXUP) return;
   ph = pf ? pf->begin(st, (w.tag + "msm_bucket_sum").c_str(), p.G) : -1;   // row/col sums + quantities
   constexpr int RW = ZK_RED_QWAVES;
   if constexpr (g2)
@@ -1008,7 +1072,8 @@ void msm_launch(MsmWork& w, const typename C::A* d_bases, const uint64_t* d_scal
                 int bits, hipStream_t st, uint32_t stride) {
   w.plan = msm_make_plan(n, bits, sw);
   const MsmSeg seg{d_bases, d_scalars, n, stride};
-  msm_launch_impl<C>(w, &seg, 1, sw, st);
+  msm_front_impl<C>(w, &seg, 1, sw, st);
+  msm_back_impl<C>(w, st, MSM_BACK_FULL, nullptr);
 }
 
 template <class C>
@@ -1017,7 +1082,8 @@ void msm_launch_shared(MsmWork& w, const typename C::A* d_bases, const uint64_t*
   w.plan = msm_make_plan_shared(n, bits, sw, c);
   if ((uint64_t)n * w.plan.nwin >= MSM_DUMMY) throw Error(ZK_ERR_ARG, "msm: too many window bases");
   const MsmSeg seg{d_bases, d_scalars, n, stride};
-  msm_launch_impl<C>(w, &seg, 1, sw, st);
+  msm_front_impl<C>(w, &seg, 1, sw, st);
+  msm_back_impl<C>(w, st, MSM_BACK_FULL, nullptr);
 }
 
 template <class C>
@@ -1026,7 +1092,25 @@ void msm_launch_batch(MsmWork& w, const MsmSeg* segs, int nseg, int bits, int c,
   w.plan = msm_make_plan_batch(segs, nseg, bits, c);
   for (int k = 0; k < nseg; k++)
     if ((uint64_t)segs[k].n * w.plan.nwin >= MSM_DUMMY) throw Error(ZK_ERR_ARG, "msm: too many window bases");
-  msm_launch_impl<C>(w, segs, nseg, 1, st);
+  msm_front_impl<C>(w, segs, nseg, 1, st);
+  msm_back_impl<C>(w, st, MSM_BACK_FULL, nullptr);
+}
+
+template <class C>
+void msm_batch_front(MsmWork& w, const MsmSeg* segs, int nseg, int bits, int c, hipStream_t st) {
+  if (nseg < 1 || nseg > MSM_MAXSEG) throw Error(ZK_ERR_ARG, "msm: batch of 1..4 MSMs");
+  w.plan = msm_make_plan_batch(segs, nseg, bits, c);
+  for (int k = 0; k < nseg; k++) {
+    const uint64_t ws = segs[k].wstride ? segs[k].wstride : segs[k].n;
+    if ((uint64_t)segs[k].ioff + segs[k].n > ws || ws * w.plan.nwin >= MSM_DUMMY)
+      throw Error(ZK_ERR_ARG, "msm: bad window-base range");
+  }
+  msm_front_impl<C>(w, segs, nseg, 1, st);
+}
+
+template <class C>
+void msm_batch_back(MsmWork& w, hipStream_t st, int mode, const MsmWork* prev) {
+  msm_back_impl<C>(w, st, mode, prev);
 }
 
 // ------------------------------------------- precomputed window bases -----
@@ -1273,6 +1357,8 @@ void host_to_abi<G2>(const host::X<host::Fq2>& p, uint64_t* w) {
   template host::X<C::HF> msm_finish<C>(const MsmWork&);                                            \
   template host::X<C::HF> msm_finish_seg<C>(const MsmWork&, int);                                   \
   template void msm_launch_batch<C>(MsmWork&, const MsmSeg*, int, int, int, hipStream_t);            \
+  template void msm_batch_front<C>(MsmWork&, const MsmSeg*, int, int, int, hipStream_t);             \
+  template void msm_batch_back<C>(MsmWork&, hipStream_t, int, const MsmWork*);                       \
   template void convert_bases<C>(const uint64_t*, C::A*, size_t, hipStream_t);                       \
   template void convert_bases_gather<C>(const uint64_t*, const uint32_t*, C::A*, size_t, hipStream_t);
 ZK_MSM_INST(G1)

@@ -71,6 +71,8 @@ struct MsmPlan {
   int shared;                       // windows share one bucket set (precomputed 2^(c w) P bases)
   int nseg;                         // batch: independent MSMs, reduction window k = MSM k
   uint32_t segshift;                // batch: bucket g belongs to MSM g >> segshift
+  int all_valid;                    // every bucket holds a value (msm_batch_back COMBINE wrote them all)
+  int quad_rc;                      // G1 row/column sums on lane quads (few sums, unsplit)
 };
 
 // One MSM of a batch (msm_launch_batch): n points, window-shifted bases
@@ -81,6 +83,10 @@ struct MsmSeg {
   const uint64_t* scalars;
   uint32_t n;
   uint32_t stride = 0;   // bytes between bases (0 = sizeof the affine point)
+  // a sub-range of a window-shifted base vector: point i of the segment is
+  // base ioff + i, and window w of it sits at w wstride + ioff + i (wstride
+  // 0 = n: the segment is the whole vector)
+  uint32_t wstride = 0, ioff = 0;
 };
 
 MsmPlan msm_make_plan(uint32_t n, int bits, int sw, int force_c = 0);
@@ -117,6 +123,18 @@ void msm_launch_shared(MsmWork& w, const typename C::A* d_bases, const uint64_t*
 // the whole batch instead of one per MSM.  msm_finish_seg(w, k) gives MSM k.
 template <class C>
 void msm_launch_batch(MsmWork& w, const MsmSeg* segs, int nseg, int bits, int c, hipStream_t st);
+// The same in two halves, for an MSM whose points arrive in parts: the
+// front (keys, sort, accumulate) and the back (bucket fixup / merge, then
+// the bucket reduction).  back modes: MSM_BACK_FULL (msm_launch_batch),
+// MSM_BACK_FIXUP (complete the buckets only: the first part of a split MSM)
+// and MSM_BACK_COMBINE (complete the buckets, add the completed buckets of
+// `prev` -- an earlier part over the same plan, already past its FIXUP back
+// on this stream or one it waited for -- then reduce: the sum of both parts).
+enum { MSM_BACK_FULL = 0, MSM_BACK_FIXUP = 1, MSM_BACK_COMBINE = 2 };
+template <class C>
+void msm_batch_front(MsmWork& w, const MsmSeg* segs, int nseg, int bits, int c, hipStream_t st);
+template <class C>
+void msm_batch_back(MsmWork& w, hipStream_t st, int mode, const MsmWork* prev);
 // d_bases[w n + i] = 2^(c w) d_bases[i] for 0 < w < W (the first n are given;
 // capacity W n).  One-time, at proving-key upload.
 template <class C>

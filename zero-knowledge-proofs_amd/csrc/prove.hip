@@ -298,7 +298,34 @@ zk_pk_dev* pk_upload(zk_ctx* ctx, const zk_pk* pk, const zk_r1cs_csr* q, uint32_
   // the a/b vectors may be shorter than V (core:171 `i < pk.a_g1.len()`): indices stay < V.
   pk_precompute_windows(ctx, *d);
   pk_witness_ranges(*d, q, own, st);
+  pk_part_cuts(*d, st);
   return d.release();
+}
+
+// out[k] = first position of idx[0, count) holding a value >= key (the idx
+// vectors ascend: compaction keeps variable order)
+__global__ void k_lower_bound(const uint32_t* __restrict__ idx, uint32_t count, uint64_t key, uint32_t* __restrict__ out) {
+  uint32_t lo = 0, hi = count;
+  while (lo < hi) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if ((uint64_t)idx[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  *out = lo;
+}
+
+void pk_part_cuts(zk_pk_dev& pk, hipStream_t st) {
+  pk.vh = pk.V / 2;
+  DevBuf d;
+  d.ensure(sizeof(uint32_t) * NUM_MSM);
+  ZK_HIP(hipMemsetAsync(d.p, 0, sizeof(uint32_t) * NUM_MSM, st));
+  for (int slot : {MSM_A, MSM_B2, MSM_B1, MSM_IC})
+    if (pk.count[slot]) {
+      k_lower_bound<<<1, 1, 0, st>>>(pk.idx[slot].as<uint32_t>(), pk.count[slot], pk.vh, d.as<uint32_t>() + slot);
+      ZK_LAUNCH_CHECK();
+    }
+  ZK_HIP(hipMemcpyAsync(pk.cut, d.p, sizeof(uint32_t) * NUM_MSM, hipMemcpyDeviceToHost, st));
+  ZK_HIP(hipStreamSynchronize(st));
 }
 
 std::vector<uint8_t> var_owner(const zk_r1cs_csr* q, uint64_t n, uint32_t N) {
@@ -510,9 +537,16 @@ static const int G1_ABI[3] = {MSM_A, MSM_B1, MSM_IC};
 // as those MSMs are done, while H is still on the GPU -- each conversion is
 // a field inversion (~40 us on one core) that would otherwise follow the
 // last MSM.
+// z_host (the drop-in host-witness prove): d_z is the ctx's device copy,
+// filled here in two parts -- variables [0, vh), then [vh, V) -- and the
+// G2 and A+B1+IC MSMs run split the same way: the first part's keys, sort
+// and accumulate start as soon as its half of z has landed, while the second
+// half is still crossing PCIe; the second part then adds the first part's
+// completed buckets (msm_batch_back COMBINE) and reduces once.
 static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, const zk_fr* r,
                              const zk_fr* s, const uint64_t* h_given = nullptr, uint32_t given_flags = 0,
-                             const std::vector<uint64_t>* ranges = nullptr, zk_proof* early = nullptr) {
+                             const std::vector<uint64_t>* ranges = nullptr, zk_proof* early = nullptr,
+                             const zk_fr* z_host = nullptr) {
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
   const auto t_start = clk::now();
@@ -523,7 +557,12 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   ctx->prof.mark_origin(st);
   const int ph_span = ctx->prof.begin(st, "prove_gpu_span", pk->n);   // first kernel .. last MSM done
   ZK_HIP(hipMemsetAsync(ctx->flags.p, 0, 16, st));
-  if (ranges) {   // every z_i < r, else ZK_ERR_ARG
+  const bool split = z_host != nullptr;
+  const uint64_t vh = split ? pk->vh : 0;
+  if (split) {   // first part of z; every z_i < r, else ZK_ERR_ARG
+    if (vh) ZK_HIP(hipMemcpyAsync(const_cast<uint64_t*>(d_z), z_host, sizeof(zk_fr) * vh, hipMemcpyHostToDevice, st));
+    check_canonical(d_z, vh, ctx->flags.as<uint32_t>(), st);
+  } else if (ranges) {   // every z_i < r, else ZK_ERR_ARG
     for (size_t k = 0; k + 1 < ranges->size(); k += 2)
       check_canonical(reinterpret_cast<const Fr*>(d_z) + (*ranges)[k], (*ranges)[k + 1] - (*ranges)[k],
                       ctx->flags.as<uint32_t>(), st);
@@ -565,6 +604,66 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       if (full) for (int k = 0; k < 4; k++) ex.v[1 + k] = full->l[k];
       k_set_extras<<<1, 64, 0, ss>>>(ctx->scal[slot].as<uint64_t>() + cnt, ex, nex);
       ZK_LAUNCH_CHECK();
+    }
+  };
+  // split parts: scalars of compacted positions [lo, hi) (+ the extras with
+  // the second part), and the segment of positions [lo, hi_with_extras)
+  auto prep_range = [&](int slot, uint32_t lo, uint32_t hi, bool extras, hipStream_t ss) {
+    const uint32_t cnt = pk->count[slot], nex = pk->extras[slot];
+    ctx->scal[slot].ensure(sizeof(uint64_t) * std::max<uint32_t>(cnt + nex, 1));
+    if (hi > lo) {
+      k_gather_lo64<<<ceil_div(hi - lo, 256), 256, 0, ss>>>(d_z, 4, pk->idx[slot].as<uint32_t>() + lo, 1u, hi - lo,
+                                                           ctx->scal[slot].as<uint64_t>() + lo);
+      ZK_LAUNCH_CHECK();
+    }
+    if (extras && nex) {
+      Extras ex{};
+      ex.v[0] = 1;
+      const zk_fr* full = slot == MSM_A ? r : slot == MSM_B2 ? s : nullptr;
+      if (full) for (int k = 0; k < 4; k++) ex.v[1 + k] = full->l[k];
+      k_set_extras<<<1, 64, 0, ss>>>(ctx->scal[slot].as<uint64_t>() + cnt, ex, nex);
+      ZK_LAUNCH_CHECK();
+    }
+  };
+  auto seg_range = [&](int slot, uint32_t lo, uint32_t hi) {
+    MsmSeg sg{pk->bases[slot].p, ctx->scal[slot].as<uint64_t>() + lo, hi - lo, pk->stride[slot]};
+    sg.wstride = pk->count[slot] + pk->extras[slot];
+    sg.ioff = lo;
+    return sg;
+  };
+  // part 0: positions [0, cut); part 1: [cut, count + extras)
+  auto launch_part = [&](int part, hipStream_t gs2, hipStream_t gsa) {
+    {
+      Range range(part ? "msm_g2_part1" : "msm_g2_part0");
+      const uint32_t c = pk->cut[MSM_B2], tot = pk->count[MSM_B2] + pk->extras[MSM_B2];
+      MsmWork& w = part ? ctx->msm[MSM_B2] : ctx->msm2[MSM_B2];
+      w.tag = serial ? (part ? "B2/" : "B2a/") : "";
+      prep_range(MSM_B2, part ? c : 0, part ? pk->count[MSM_B2] : c, part == 1, gs2);
+      const MsmSeg sg = seg_range(MSM_B2, part ? c : 0, part ? tot : c);
+      msm_batch_front<G2>(w, &sg, 1, 64, pk->win_c, gs2);
+      msm_batch_back<G2>(w, gs2, part ? MSM_BACK_COMBINE : MSM_BACK_FIXUP, part ? &ctx->msm2[MSM_B2] : nullptr);
+      if (part) {
+        msm_download<G2>(w, gs2);
+        ZK_HIP(hipEventRecord(ctx->ev_done[MSM_B2], gs2));
+      }
+    }
+    {
+      Range range(part ? "msm_g1_a_b1_ic_part1" : "msm_g1_a_b1_ic_part0");
+      MsmSeg segs[3];
+      for (int i = 0; i < 3; i++) {
+        const int sl = G1_ABI[i];
+        const uint32_t c = pk->cut[sl], tot = pk->count[sl] + pk->extras[sl];
+        prep_range(sl, part ? c : 0, part ? pk->count[sl] : c, part == 1, gsa);
+        segs[i] = seg_range(sl, part ? c : 0, part ? tot : c);
+      }
+      MsmWork& w = part ? ctx->msm[MSM_A] : ctx->msm2[MSM_A];
+      w.tag = serial ? (part ? "ABI/" : "ABIa/") : "";
+      msm_batch_front<G1>(w, segs, 3, 64, pk->win_c, gsa);
+      msm_batch_back<G1>(w, gsa, part ? MSM_BACK_COMBINE : MSM_BACK_FIXUP, part ? &ctx->msm2[MSM_A] : nullptr);
+      if (part) {
+        msm_download<G1>(w, gsa);
+        ZK_HIP(hipEventRecord(ctx->ev_done[MSM_A], gsa));
+      }
     }
   };
   static const char* const tags[NUM_MSM] = {"A/", "B2/", "B1/", "IC/", "H/"};
@@ -613,7 +712,28 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   };
   // MSMs first, then the quotient (enqueueing the quotient first measured
   // 0.37 ms slower: profiles/r03_ab_quotient_first_rejected.txt)
-  launch_msms();
+  if (split) {
+    if (!serial) {
+      ZK_HIP(hipStreamWaitEvent(s_g2, ctx->ev_scal, 0));
+      ZK_HIP(hipStreamWaitEvent(s_abi, ctx->ev_scal, 0));
+    }
+    launch_part(0, s_g2, s_abi);
+    // second part of z (the host thread waits for the pageable copy while
+    // the GPU runs the first part's MSMs), then its MSMs
+    const uint64_t V = pk->V;
+    if (V > vh)
+      ZK_HIP(hipMemcpyAsync(const_cast<uint64_t*>(d_z) + 4 * vh, z_host + vh, sizeof(zk_fr) * (V - vh),
+                            hipMemcpyHostToDevice, st));
+    check_canonical(d_z + 4 * vh, V - vh, ctx->flags.as<uint32_t>(), st);
+    ZK_HIP(hipEventRecord(ctx->ev_scal, st));
+    if (!serial) {
+      ZK_HIP(hipStreamWaitEvent(s_g2, ctx->ev_scal, 0));
+      ZK_HIP(hipStreamWaitEvent(s_abi, ctx->ev_scal, 0));
+    }
+    launch_part(1, s_g2, s_abi);
+  } else {
+    launch_msms();
+  }
   run_quotient();
   // the exchange watchdog below counts from here: a host-staged exchange has
   // finished its all-to-alls inside run_quotient, and only local GPU work
@@ -712,14 +832,14 @@ static int combine(const Partial* parts, size_t k, zk_proof* out) {
 }
 
 int prove_impl(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_z, size_t zlen, size_t num_public,
-               const zk_fr* r, const zk_fr* s, zk_proof* out) {
+               const zk_fr* r, const zk_fr* s, zk_proof* out, const zk_fr* z_host) {
   // Witness::new (core:81-99) and the length check of validate (core:113-118)
   if (!fr_canonical(*r) || !fr_canonical(*s)) return ZK_ERR_ARG;   // Fr::rand draws are reduced
   if (num_public >= zlen) return ZK_ERR_INVALID_WITNESS;
   if (zlen != pk->V) return ZK_ERR_INVALID_WITNESS;
   if (pk->nshards != 1) return ZK_ERR_ARG;
   zk_proof ab{};
-  Partial p = prove_partial(ctx, pk, reinterpret_cast<const uint64_t*>(d_z), r, s, nullptr, 0, nullptr, &ab);
+  Partial p = prove_partial(ctx, pk, reinterpret_cast<const uint64_t*>(d_z), r, s, nullptr, 0, nullptr, &ab, z_host);
   if (p.status != ZK_OK) return p.status;
   // combine() for one part: pi_A, pi_B already converted; pi_C = IC + H + s A + r B1
   out->a = ab.a;

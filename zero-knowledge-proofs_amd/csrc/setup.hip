@@ -564,6 +564,7 @@ int setup_impl(zk_ctx* ctx, const zk_r1cs_csr* q, const zk_setup_params* P, uint
   build_slot(MSM_H, false, hh, sh, n, 0, none, 0, /*strided*/ true);
   pk_precompute_windows(ctx, *d);
   pk_witness_ranges(*d, q, own, st);
+  pk_part_cuts(*d, st);
   *pk_dev = d.release();
   return ZK_OK;
 }

@@ -329,7 +329,7 @@ def cpu_sample_baseline(zkp, ctx, log_n, params, r, s, seed):
             "bit_exact_vs_gpu": bool(np.array_equal(gpu.words, proof))}
 
 
-def anchor_bench(zkp, ctx, log_n, params, r, s, seed, steps, warmup):
+def anchor_bench(zkp, ctx, log_n, params, r, s, seed, steps, warmup, win_c=0):
     """The N = 1 line's strong-scaling anchor: the SAME workload the N > 1
     lines shard (configs[4], 2^log_n constraints) proved on this one GPU,
     overlapped schedule timed like the headline, plus a serial-schedule pass
@@ -340,7 +340,11 @@ def anchor_bench(zkp, ctx, log_n, params, r, s, seed, steps, warmup):
     zlen = 3 * n + 1
     qap = zkp.QAP(zkp.CSRMatrices.synthetic(n))
     t0 = time.perf_counter()
-    dpk = zkp.CRS.generate_device(ctx, qap, zkp.SetupParams(*params), 1)
+    ctx.set_option(zkp.ZK_OPT_PROVE_WIN_C, win_c)   # 0: the library's choice by size
+    try:
+        dpk = zkp.CRS.generate_device(ctx, qap, zkp.SetupParams(*params), 1)
+    finally:
+        ctx.set_option(zkp.ZK_OPT_PROVE_WIN_C, 0)
     t_setup = time.perf_counter() - t0
     d_z = ctx.synthetic_witness(n, seed + 1)
     try:
@@ -379,7 +383,8 @@ def anchor_bench(zkp, ctx, log_n, params, r, s, seed, steps, warmup):
                          "g1_pairs": g1, "g2_pairs": g2,
                          "timing": "HIP events around every MSM kernel (sort, accumulate, merge, bucket sums) of "
                                    "serial-schedule proves (zk_ctx_set_schedule 3), per proof"},
-            "roofline": roofline_from(prof, log_n),
+            "window_bits": win_c or (22 if n >= 1 << 24 else 16),
+            "roofline": roofline_from(prof, log_n) if not win_c else None,
             "proof_compressed": hexp,
             "bit_exact_vs_oracle": (hexp == pinned) if pinned else None,
             "oracle_reference": "bench.ORACLE_2P24 (pinned oracle proof; tests/test_gpu_2p24.py reruns the oracle)"
@@ -894,8 +899,16 @@ def main():
         if args.anchor_log_n:
             log(f"[bench] strong-scaling anchor: 2^{args.anchor_log_n} prove on this GPU")
             torch.cuda.empty_cache()
-            extra["strong_scaling_anchor"] = anchor_bench(zkp, ctx, args.anchor_log_n, params, r, s, args.seed,
-                                                          args.steps, args.warmup)
+            anc = anchor_bench(zkp, ctx, args.anchor_log_n, params, r, s, args.seed, args.steps, args.warmup)
+            if args.anchor_log_n >= 24:
+                # the same circuit with the N > 1 shards' window plan (c = 16,
+                # 4 windows): MSM scaling at an equal plan
+                torch.cuda.empty_cache()
+                c16 = anchor_bench(zkp, ctx, args.anchor_log_n, params, r, s, args.seed, max(2, args.steps // 2),
+                                   1, win_c=16)
+                anc["same_plan_c16"] = {k: c16[k] for k in ("ms_per_step", "value", "msm_only", "window_bits",
+                                                            "bit_exact_vs_oracle")}
+            extra["strong_scaling_anchor"] = anc
     if rank == 0:
         if world == 1:
             workload = f"groth16_prove_2^{log_n_total}"

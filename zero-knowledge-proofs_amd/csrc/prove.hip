@@ -314,8 +314,17 @@ __global__ void k_lower_bound(const uint32_t* __restrict__ idx, uint32_t count, 
   *out = lo;
 }
 
+// The first part of a host witness is 1/ZK_HOST_SPLIT_DIV of it: its MSM
+// share then starts after a third of the copy and still outlasts the rest
+// of it.  Host-witness minus device-witness prove at 2^20 (medians of 3,
+// tools/pcie_ab.py, profiles/r04_ab_host_split.txt): 1/2 +1.33 ms, 1/3
+// +0.84, 1/4 +0.86, 1/6 +1.29; one whole copy before the prove was +2.5.
+// (ZK_HOST_SPLIT_DIV: A/B builds only, tools/build_variant.sh.)
+#ifndef ZK_HOST_SPLIT_DIV
+#define ZK_HOST_SPLIT_DIV 3
+#endif
 void pk_part_cuts(zk_pk_dev& pk, hipStream_t st) {
-  pk.vh = pk.V / 2;
+  pk.vh = pk.V / ZK_HOST_SPLIT_DIV;
   DevBuf d;
   d.ensure(sizeof(uint32_t) * NUM_MSM);
   ZK_HIP(hipMemsetAsync(d.p, 0, sizeof(uint32_t) * NUM_MSM, st));

@@ -25,7 +25,8 @@ key and the witness already resident in HBM.
          fold.  Beside the timed value: `msm_only` (max over ranks of the MSM
          kernels' time per proof, serial schedule), `roofline` (rank 0's
          accumulate), `quotient_replicated` (same keys, every rank computing
-         the whole quotient, no all-to-all) and `cpu_baseline` (the oracle on
+         the whole quotient, no all-to-all), `exchange_first` (the MSMs
+         waiting for the distributed quotient) and `cpu_baseline` (the oracle on
          a bounded sample, rank 0).  --scaling weak keeps 2^log_n constraints
          per GPU instead.
 
@@ -818,29 +819,41 @@ def main():
             extra["serial_schedule"] = {"ms_per_step": round(float(mx[1]) * 1e3, 3), "steps": ks}
             if rank == 0:
                 roofline = roofline_from(serial_prof, log_n_total, overlapped=prof, nshards=world)
-        # the replicated alternative on the same keys: every rank computes the
-        # whole quotient (ZK_OPT_DIST_QUOTIENT 0), no all-to-all
-        if quotient_mode.startswith("distributed"):
-            ctx.set_option(zkp.ZK_OPT_DIST_QUOTIENT, 0)
+        def timed_alternative(option, value, default):
+            """ms per step (max over ranks) of the same proof with one ctx
+            option changed; the proof must not change"""
+            ctx.set_option(option, value)
             step()
             torch.cuda.synchronize()
             dist.barrier()
             t0 = time.perf_counter()
             for _ in range(args.steps):
-                pr = step()
+                pa = step()
             torch.cuda.synchronize()
             dist.barrier()
-            t_rep = torch.tensor([(time.perf_counter() - t0) / args.steps], dtype=torch.float64, device=coll_dev)
-            dist.all_reduce(t_rep, op=dist.ReduceOp.MAX)
-            ctx.set_option(zkp.ZK_OPT_DIST_QUOTIENT, -1)
-            if pr != proof:
-                raise SystemExit("replicated-quotient proof differs from the distributed one")
-            extra["quotient_replicated"] = {
-                "ms_per_step": round(float(t_rep[0]) * 1e3, 3), "value": round(n / float(t_rep[0]), 1),
-                "unit": "constraints/s",
-                "note": "same keys and witness, every rank computing the whole 2^%d quotient "
-                        "(zk_ctx_set_option ZK_OPT_DIST_QUOTIENT 0) instead of the three all-to-alls; "
-                        "the line's value is the distributed mode" % log_n_total}
+            t_alt = torch.tensor([(time.perf_counter() - t0) / args.steps], dtype=torch.float64, device=coll_dev)
+            dist.all_reduce(t_alt, op=dist.ReduceOp.MAX)
+            ctx.set_option(option, default)
+            if pa != proof:
+                raise SystemExit(f"proof with option {option} = {value} differs from the default one")
+            return {"ms_per_step": round(float(t_alt[0]) * 1e3, 3), "value": round(n / float(t_alt[0]), 1),
+                    "unit": "constraints/s"}
+        if quotient_mode.startswith("distributed"):
+            # the replicated alternative on the same keys: every rank computes
+            # the whole quotient (ZK_OPT_DIST_QUOTIENT 0), no all-to-all
+            extra["quotient_replicated"] = dict(
+                timed_alternative(zkp.ZK_OPT_DIST_QUOTIENT, 0, -1),
+                note="same keys and witness, every rank computing the whole 2^%d quotient "
+                     "(zk_ctx_set_option ZK_OPT_DIST_QUOTIENT 0) instead of the three all-to-alls; "
+                     "the line's value is the distributed mode" % log_n_total)
+            # the other order: the quotient and its all-to-alls first, the G2
+            # and A+B1+IC MSMs after them (ZK_OPT_EXCHANGE_FIRST 1)
+            extra["exchange_first"] = dict(
+                timed_alternative(zkp.ZK_OPT_EXCHANGE_FIRST, 1, 0),
+                note="same keys and witness, the G2 and A+B1+IC MSMs waiting for the distributed quotient "
+                     "(zk_ctx_set_option ZK_OPT_EXCHANGE_FIRST 1) so that its all-to-alls never queue behind "
+                     "a full-occupancy accumulate; the line's value is the default order (MSMs start with "
+                     "the witness)")
         if not args.no_cpu_baseline:
             if rank == 0:
                 log(f"[bench] CPU baseline: oracle 2^{args.cpu_sample_log_n} sample on rank 0")

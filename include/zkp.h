@@ -154,10 +154,18 @@ int zk_ctx_set_schedule(zk_ctx *ctx, int schedule);
  *                         rank computes the whole quotient and reads the
  *                         whole witness (the replicated alternative, for
  *                         measuring one against the other on one node)
+ *   ZK_OPT_EXCHANGE_FIRST 0 (default): a distributed-quotient proof starts
+ *                         its G2 and A+B1+IC MSMs with the witness, beside
+ *                         the quotient and its three all-to-alls; 1: those
+ *                         MSMs wait until the quotient (all-to-alls
+ *                         included) is done, so the collectives never queue
+ *                         behind a full-occupancy accumulate (for measuring
+ *                         one order against the other on one node; no
+ *                         effect without a distributed quotient)
  * (Test hooks -- the virtual-rank prove, the bare exchange, fault injection
  * -- live in a separate library, include/zkp_test.h.) */
 enum { ZK_OPT_QUOTIENT_PATH = 1, ZK_OPT_PROVE_WIN_C = 2, ZK_OPT_EXCHANGE_TIMEOUT_MS = 3,
-       ZK_OPT_DIST_QUOTIENT = 5 };
+       ZK_OPT_DIST_QUOTIENT = 5, ZK_OPT_EXCHANGE_FIRST = 6 };
 int zk_ctx_set_option(zk_ctx *ctx, int option, int64_t value);
 
 /* ---------------------------------------------------------------- MSM --- */

@@ -52,6 +52,7 @@ def test_bench_two_rank_path_matches_single_gpu(ctx, zkp):
     roof = rec["roofline"]
     assert roof["kernel"] == "k_msm_accum<G1>" and 0 < roof["frac"] < 1 and roof["avg_launch_ms"] > 0
     assert rec["quotient_replicated"]["ms_per_step"] > 0
+    assert rec["exchange_first"]["ms_per_step"] > 0
     cb = rec["cpu_baseline"]
     assert cb["value"] > 0 and cb["bit_exact_vs_gpu"] and cb["cores"] >= 1
     sys.path.insert(0, ROOT)

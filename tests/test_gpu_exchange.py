@@ -19,7 +19,8 @@ the 8-GPU run takes (only ncclAllToAll itself differs).
   * a rank passing a witness slice of the wrong length fails on EVERY rank
     with ZK_ERR_ARG (the status agreement), and the exchange stays usable;
   * ZK_OPT_DIST_QUOTIENT = 0 (each rank the whole quotient, whole witness)
-    gives the same partial as the distributed quotient;
+    gives the same partial as the distributed quotient, and so does
+    ZK_OPT_EXCHANGE_FIRST = 1 (the MSMs waiting for the quotient);
   * a non-canonical value in a variable no row references (so no stage reads
     it) is still rejected by the rank var_owner gives it."""
 import json
@@ -93,6 +94,11 @@ def _worker(rank, world, port, log_n, seed, out_dir, mode):
         res["replicated_ranges"] = [[int(a), int(b)] for a, b in dpk.witness_ranges()]
         res["replicated_equal"] = zkp.Prover.prove_partial_host(dpk, dpk.witness_slice(z), len(z), 1, r, s) == part
         ctx.set_option(zkp.ZK_OPT_DIST_QUOTIENT, -1)
+        # the quotient and its all-to-alls before the MSMs: same partial
+        ctx.set_option(zkp.ZK_OPT_EXCHANGE_FIRST, 1)
+        res["exchange_first_equal"] = (zkp.Prover.prove_partial_host(dpk, zs, len(z), 1, r, s) == part and
+                                       zkp.Prover.prove_partial(dpk, dz.data_ptr(), len(z), 1, r, s) == part)
+        ctx.set_option(zkp.ZK_OPT_EXCHANGE_FIRST, 0)
         # one extra variable that no row references, holding r (non-canonical)
         csr = zkp.CSRMatrices.synthetic(n)
         qx = zkp.QAP(zkp.CSRMatrices(n, 3 * n + 2, csr.mats))
@@ -173,7 +179,7 @@ def test_rank_failure_mid_quotient_aborts_peers(oracle, tmp_path):
 
 
 @pytest.mark.timeout(300)
-def test_slice_errors_replicated_quotient_and_unreferenced_variable(oracle, tmp_path):
+def test_slice_errors_replicated_quotient_exchange_first_and_unreferenced_variable(oracle, tmp_path):
     log_n, seed = 10, 2718
     res = _run(tmp_path, 2, log_n, seed, "edge")
     assert res[0]["proof"] == _oracle_proof(oracle, log_n, seed)
@@ -182,6 +188,7 @@ def test_slice_errors_replicated_quotient_and_unreferenced_variable(oracle, tmp_
         assert r["short_slice_error"] == "ValueError", r      # both ranks, through the agreement
         assert r["after_short_equal"], r                       # the exchange survived
         assert r["replicated_ranges"] == [[0, zlen]] and r["replicated_equal"], r
+        assert r["exchange_first_equal"], r
     # var_owner gives the unreferenced variable (index 3n+1 of 3n+2) to rank 1
     assert res[1]["extra_in_ranges"] and res[1]["extra_error"] == "ValueError", res[1]
     assert not res[0]["extra_in_ranges"] and res[0]["extra_error"] is None, res[0]

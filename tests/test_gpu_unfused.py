@@ -63,6 +63,7 @@ def test_options_reject_unknown_values(zkp):
     with zkp.Context(0) as ctx:
         # 4: the old fault-injection option, now only in libzkp_amd_test.so
         for opt, val in ((zkp.ZK_OPT_QUOTIENT_PATH, 2), (zkp.ZK_OPT_PROVE_WIN_C, 17), (zkp.ZK_OPT_DIST_QUOTIENT, 1),
+                         (zkp.ZK_OPT_EXCHANGE_FIRST, 2), (zkp.ZK_OPT_EXCHANGE_FIRST, -1),
                          (4, 2), (99, 0)):
             with pytest.raises(ValueError):
                 ctx.set_option(opt, val)

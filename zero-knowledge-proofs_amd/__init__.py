@@ -57,6 +57,7 @@ EXPORTS = (
 TEST_EXPORTS = ("zk_test_prove_virtual_shards", "zk_test_exchange", "zk_test_fault_after_exchange",
                 "zk_test_pk_bases", "zk_test_pk_info")
 ZK_OPT_QUOTIENT_PATH, ZK_OPT_PROVE_WIN_C, ZK_OPT_EXCHANGE_TIMEOUT_MS, ZK_OPT_DIST_QUOTIENT = 1, 2, 3, 5
+ZK_OPT_EXCHANGE_FIRST = 6
 CSRC = os.path.join(_HERE, "csrc")
 
 
@@ -369,9 +370,11 @@ class Context:
     def set_option(self, option, value):
         """zk_ctx_set_option: ZK_OPT_QUOTIENT_PATH (-1 by size, 0 small-domain,
         1 large-domain), ZK_OPT_PROVE_WIN_C (0 by size, 16, 22; keys made
-        afterwards), ZK_OPT_EXCHANGE_TIMEOUT_MS (>= 1) or ZK_OPT_DIST_QUOTIENT
+        afterwards), ZK_OPT_EXCHANGE_TIMEOUT_MS (>= 1), ZK_OPT_DIST_QUOTIENT
         (-1 distributed when an exchange of the key's shape is attached, 0
-        replicated).  Explicit path choices for tests and A/B runs."""
+        replicated) or ZK_OPT_EXCHANGE_FIRST (0 MSMs start with the witness, 1
+        they wait for the distributed quotient).  Explicit path choices for
+        tests and A/B runs."""
         _check(lib().zk_ctx_set_option(C.c_void_p(self._h), C.c_int(int(option)), C.c_int64(int(value))), self,
                "zk_ctx_set_option")
 

@@ -63,6 +63,7 @@ zk_ctx* zk_ctx_create(int device) {
     for (int i = 0; i < NUM_SIDE; i++)
       ZK_HIP(hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking, i == 0 ? hi_prio : lo_prio));
     ZK_HIP(hipEventCreateWithFlags(&c->ev_scal, hipEventDisableTiming));
+    ZK_HIP(hipEventCreateWithFlags(&c->ev_quot, hipEventDisableTiming));
     for (auto& e : c->ev_done) ZK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     return c.release();
   } catch (...) {
@@ -79,6 +80,7 @@ void zk_ctx_destroy(zk_ctx* ctx) {
   for (int i = 0; i < NUM_SIDE; i++) (void)hipStreamDestroy(ctx->side[i]);
   (void)hipStreamDestroy(ctx->stream);
   (void)hipEventDestroy(ctx->ev_scal);
+  (void)hipEventDestroy(ctx->ev_quot);
   for (auto& e : ctx->ev_done) (void)hipEventDestroy(e);
   delete ctx;
 }

@@ -30,6 +30,7 @@ struct zk_ctx {
   hipStream_t stream = nullptr;                 // main stream
   hipStream_t side[zk::NUM_SIDE] = {};          // G2 / IC / A+B1 MSM streams
   hipEvent_t ev_scal = nullptr;                 // witness checked (flags reset)
+  hipEvent_t ev_quot = nullptr;                 // quotient done (ZK_OPT_EXCHANGE_FIRST)
   hipEvent_t ev_done[zk::NUM_MSM] = {};         // per-MSM completion (results downloaded)
   std::string err;
   zk::MsmWork msm[zk::NUM_MSM];
@@ -51,6 +52,7 @@ struct zk_ctx {
   double exch_timeout_ms = 60000;              // watchdog of an attached exchange
   int dist_quotient = -1;                      // -1 distributed when an exchange of the key's shape
                                                // is attached, 0 never (each rank the whole quotient)
+  int exchange_first = 0;                      // 1: distributed proofs run the quotient before the MSMs
 
   zk::NttDomain& domain(uint32_t log_n);
 };

@@ -720,7 +720,17 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
     }
   };
   // MSMs first, then the quotient (enqueueing the quotient first measured
-  // 0.37 ms slower: profiles/r03_ab_quotient_first_rejected.txt)
+  // 0.37 ms slower: profiles/r03_ab_quotient_first_rejected.txt).  With
+  // ZK_OPT_EXCHANGE_FIRST a distributed quotient goes first and the side
+  // streams wait for it, so its all-to-alls find free CUs on every rank.
+  // (Split uploads are single-GPU only: the quotient needs all of z.)
+  const bool xfirst = dist && ctx->exchange_first == 1 && !serial && !split;
+  if (xfirst) {
+    run_quotient();
+    ZK_HIP(hipEventRecord(ctx->ev_quot, st));
+    ZK_HIP(hipStreamWaitEvent(s_g2, ctx->ev_quot, 0));
+    ZK_HIP(hipStreamWaitEvent(s_abi, ctx->ev_quot, 0));
+  }
   if (split) {
     if (!serial) {
       ZK_HIP(hipStreamWaitEvent(s_g2, ctx->ev_scal, 0));
@@ -743,7 +753,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   } else {
     launch_msms();
   }
-  run_quotient();
+  if (!xfirst) run_quotient();
   // the exchange watchdog below counts from here: a host-staged exchange has
   // finished its all-to-alls inside run_quotient, and only local GPU work
   // (RCCL: the enqueued collectives) is left

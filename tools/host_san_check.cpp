@@ -69,6 +69,28 @@ int main() {
   if (pairing_product_is_one(ps, qs)) return 6;
   (void)qx0;
   (void)qy0;
+  // divstep inversion == Fermat, on 0, 1, m - 1 and 2000 pseudo-random values
+  {
+    uint64_t st = 0x9e3779b97f4a7c15ull;
+    for (int k = 0; k < 2003; k++) {
+      Fq a = zero();
+      if (k == 1) a = one();
+      else if (k == 2) a = neg(one());
+      else if (k > 2) {
+        for (int i = 0; i < 6; i++) {
+          st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+          a.l[i] = st;
+        }
+        a.l[5] &= 0x0fffffffffffffffull;   // < 2^380 < m
+      }
+      const Fq x = inv(a), y = inv_fermat(a);
+      if (std::memcmp(&x, &y, sizeof x) != 0) return 7;
+      if (k) {
+        const Fq o = mul(a, x), u = one();
+        if (std::memcmp(&o, &u, sizeof o) != 0) return 8;
+      }
+    }
+  }
   std::printf("host sanitizer check ok\n");
   return 0;
 }

@@ -175,7 +175,9 @@ inline Fq sqr(const Fq& a) { return mul(a, a); }
 inline Fq neg(const Fq& a) { Fq z{}; return sub(z, a); }
 inline Fq one() { Fq r; memcpy(r.l, FQ().one, 48); return r; }
 inline Fq zero() { Fq r{}; return r; }
-inline Fq inv(const Fq& a) {
+// a^(m-2) (Fermat): 384 squarings + ~190 products, ~40 us on one core.
+// Kept as the reference for inv() below.
+inline Fq inv_fermat(const Fq& a) {
   uint64_t e[6]; memcpy(e, FQ_M, 48);
   e[0] -= 2;  // m is odd and > 2
   Fq acc = one();
@@ -184,6 +186,140 @@ inline Fq inv(const Fq& a) {
     if ((e[i >> 6] >> (i & 63)) & 1) acc = mul(acc, a);
   }
   return acc;
+}
+
+// Constant-time inversion by Bernstein-Yang divsteps (the safegcd form with
+// zeta = -(delta + 1/2)), 62 divsteps per round on the low words of (f, g),
+// each round's 2x2 transition matrix (entries |.| <= 2^62) then applied to the
+// full f, g and to the Bezout coefficients d, e, which stay in (-2m, m) by
+// adding the multiple of m that makes them divisible by 2^62.  Numbers are 7
+// signed 62-bit limbs (434 bits; the top limb carries the sign).  A 381-bit
+// modulus needs at most (49 * 381 + 57) / 17 = 1101 divsteps: 18 rounds.
+// About 10x fewer cycles than Fermat; it sits on the proof's critical path
+// (pi_C's affine conversion follows the last MSM).
+namespace bgcd {
+constexpr int L = 7, ROUNDS = 18;
+constexpr uint64_t M62 = ~0ull >> 2;
+typedef __int128 i128;
+struct S62 { int64_t v[L]; };
+inline S62 from_words(const uint64_t (&w)[6]) {
+  S62 s;
+  for (int i = 0; i < L; i++) {
+    const int bit = 62 * i, k = bit >> 6, sh = bit & 63;
+    uint64_t x = k < 6 ? w[k] >> sh : 0;
+    if (sh > 2 && k + 1 < 6) x |= w[k + 1] << (64 - sh);
+    s.v[i] = (int64_t)(x & M62);
+  }
+  return s;
+}
+struct Consts {
+  S62 m;
+  uint64_t minv62;   // m^-1 mod 2^62
+};
+inline const Consts& consts() {
+  static const Consts c = [] {
+    Consts k;
+    uint64_t w[6];
+    memcpy(w, FQ_M, 48);
+    k.m = from_words(w);
+    uint64_t x = 1;
+    for (int i = 0; i < 7; i++) x *= 2 - FQ_M[0] * x;
+    k.minv62 = x & M62;
+    return k;
+  }();
+  return c;
+}
+inline int64_t divsteps62(int64_t zeta, uint64_t f, uint64_t g, int64_t (&t)[4]) {
+  uint64_t u = 1, v = 0, q = 0, r = 1;
+  for (int i = 0; i < 62; i++) {
+    const uint64_t c1 = (uint64_t)(zeta >> 63);   // zeta < 0
+    const uint64_t c2 = 0 - (g & 1);              // g odd
+    const uint64_t x = (f ^ c1) - c1, y = (u ^ c1) - c1, z = (v ^ c1) - c1;
+    g += x & c2; q += y & c2; r += z & c2;
+    const uint64_t c3 = c1 & c2;
+    zeta = (zeta ^ (int64_t)c3) - 1;
+    f += g & c3; u += q & c3; v += r & c3;
+    g >>= 1; u <<= 1; v <<= 1;
+  }
+  t[0] = (int64_t)u; t[1] = (int64_t)v; t[2] = (int64_t)q; t[3] = (int64_t)r;
+  return zeta;
+}
+// (f, g) <- (u f + v g, q f + r g) / 2^62, exact
+inline void update_fg(S62& f, S62& g, const int64_t (&t)[4]) {
+  i128 cf = (i128)t[0] * f.v[0] + (i128)t[1] * g.v[0];
+  i128 cg = (i128)t[2] * f.v[0] + (i128)t[3] * g.v[0];
+  cf >>= 62; cg >>= 62;
+  for (int i = 1; i < L; i++) {
+    cf += (i128)t[0] * f.v[i] + (i128)t[1] * g.v[i];
+    cg += (i128)t[2] * f.v[i] + (i128)t[3] * g.v[i];
+    f.v[i - 1] = (int64_t)((uint64_t)cf & M62); cf >>= 62;
+    g.v[i - 1] = (int64_t)((uint64_t)cg & M62); cg >>= 62;
+  }
+  f.v[L - 1] = (int64_t)cf;
+  g.v[L - 1] = (int64_t)cg;
+}
+// (d, e) <- (u d + v e, q d + r e) / 2^62 mod m, in (-2m, m) -> (-2m, m)
+inline void update_de(S62& d, S62& e, const int64_t (&t)[4]) {
+  const Consts& K = consts();
+  const int64_t u = t[0], v = t[1], q = t[2], r = t[3];
+  const int64_t sd = d.v[L - 1] >> 63, se = e.v[L - 1] >> 63;
+  int64_t md = (u & sd) + (v & se), me = (q & sd) + (r & se);
+  i128 cd = (i128)u * d.v[0] + (i128)v * e.v[0];
+  i128 ce = (i128)q * d.v[0] + (i128)r * e.v[0];
+  md -= (int64_t)((K.minv62 * (uint64_t)cd + (uint64_t)md) & M62);
+  me -= (int64_t)((K.minv62 * (uint64_t)ce + (uint64_t)me) & M62);
+  cd += (i128)K.m.v[0] * md;
+  ce += (i128)K.m.v[0] * me;
+  cd >>= 62; ce >>= 62;
+  for (int i = 1; i < L; i++) {
+    cd += (i128)u * d.v[i] + (i128)v * e.v[i] + (i128)K.m.v[i] * md;
+    ce += (i128)q * d.v[i] + (i128)r * e.v[i] + (i128)K.m.v[i] * me;
+    d.v[i - 1] = (int64_t)((uint64_t)cd & M62); cd >>= 62;
+    e.v[i - 1] = (int64_t)((uint64_t)ce & M62); ce >>= 62;
+  }
+  d.v[L - 1] = (int64_t)cd;
+  e.v[L - 1] = (int64_t)ce;
+}
+// d in (-2m, m), times the sign of f (+-1) -> [0, m) as 6 words
+inline void to_words(S62 d, int64_t fsign, uint64_t (&w)[6]) {
+  const Consts& K = consts();
+  for (int pass = 0; pass < 3; pass++) {
+    const int64_t sg = pass == 1 ? fsign : d.v[L - 1] >> 63;
+    i128 c = 0;
+    for (int i = 0; i < L; i++) {
+      if (pass == 1) c += (i128)((d.v[i] ^ sg) - sg);
+      else c += (i128)d.v[i] + (i128)(K.m.v[i] & sg);
+      d.v[i] = i + 1 < L ? (int64_t)((uint64_t)c & M62) : (int64_t)c;
+      c >>= 62;
+    }
+  }
+  for (int k = 0; k < 6; k++) {
+    const int bit = 64 * k, i = bit / 62, sh = bit - 62 * i;
+    uint64_t x = (uint64_t)d.v[i] >> sh;
+    if (i + 1 < L) x |= (uint64_t)d.v[i + 1] << (62 - sh);
+    if (sh > 60 && i + 2 < L) x |= (uint64_t)d.v[i + 2] << (124 - sh);
+    w[k] = x;
+  }
+}
+}  // namespace bgcd
+
+// Montgomery form in and out: canonical(a R)^-1 = a^-1 R^-1, times R^2
+// twice.  0 -> 0 (as Fermat).
+inline Fq inv(const Fq& a) {
+  using namespace bgcd;
+  S62 f = consts().m, g = from_words(a.l), d{}, e{};
+  e.v[0] = 1;
+  int64_t zeta = -1;
+  for (int k = 0; k < ROUNDS; k++) {
+    int64_t t[4];
+    zeta = divsteps62(zeta, (uint64_t)f.v[0], (uint64_t)g.v[0], t);
+    update_de(d, e, t);
+    update_fg(f, g, t);
+  }
+  Fq o, r2;
+  to_words(d, f.v[L - 1] >> 63, o.l);
+  memcpy(r2.l, FQ().r2, 48);
+  return mul(mul(o, r2), r2);
 }
 inline Fq from_mont(const Fq& a) { Fq o{}; o.l[0] = 1; return mul(a, o); }
 // host Montgomery (R = 2^384) <-> device Montgomery (R = 2^392), see constants.hpp

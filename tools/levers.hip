@@ -423,6 +423,39 @@ __global__ void k_compare(const G1X* __restrict__ xs, const G1A* __restrict__ as
   ok[c] = (fp_eq(x, a.x) && fp_eq(y, a.y)) ? 1u : 0u;
 }
 
+// s P + r Q on ONE wave (the pi_C term s pi_A + r B1 moved to the GPU, as a
+// latency measurement): 4-bit Straus, 2 x 15 table adds, 256 doublings and
+// up to 128 adds, tables in global memory per lane (each lane computes the
+// same term)
+__global__ void __launch_bounds__(64) k_straus(const G1A* __restrict__ pts, uint4 ka, uint4 kb, uint4 kc, uint4 kd,
+                                               G1X* __restrict__ tab, G1X* __restrict__ out) {
+  const uint32_t lane = threadIdx.x;
+  G1X* tp = tab + lane * 32;
+  G1X* tq = tp + 16;
+  const G1A P = ld_vec(&pts[1]), Q = ld_vec(&pts[2]);
+  G1X t;
+  xyzz_set_inf(t);
+  st_vec(&tp[0], t);
+  st_vec(&tq[0], t);
+  t = xyzz_from_aff(P);
+  st_vec(&tp[1], t);
+  for (int i = 2; i < 16; i++) { t = xyzz_madd(t, P); st_vec(&tp[i], t); }
+  t = xyzz_from_aff(Q);
+  st_vec(&tq[1], t);
+  for (int i = 2; i < 16; i++) { t = xyzz_madd(t, Q); st_vec(&tq[i], t); }
+  const uint32_t k1[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
+  const uint32_t k2[8] = {kc.x, kc.y, kc.z, kc.w, kd.x, kd.y, kd.z, kd.w};
+  G1X acc;
+  xyzz_set_inf(acc);
+  for (int w = 63; w >= 0; w--) {
+    for (int d = 0; d < 4; d++) acc = xyzz_dbl(acc);
+    const uint32_t d1 = (k1[w >> 3] >> ((w & 7) * 4)) & 15u, d2 = (k2[w >> 3] >> ((w & 7) * 4)) & 15u;
+    if (d1) acc = xyzz_add(acc, ld_vec(&tp[d1]));
+    if (d2) acc = xyzz_add(acc, ld_vec(&tq[d2]));
+  }
+  st_vec(&out[lane], acc);
+}
+
 // ------------------------------------------------------------- host ------
 static int g_cus = 0;
 static FILE* g_adds = nullptr;
@@ -612,6 +645,18 @@ int main(int argc, char** argv) {
     ms = time_launch([&] { k_inv_chain<INV_FERMAT><<<T / 128, 128>>>(pts, MASK, 2, T, f1); });
     note("k_inv_chain<1>", (double)T * 2);
     res.push_back({"inversion fermat (G inv/s)", ms, (double)T * 2 / ms / 1e6, wps, vg});
+  }
+  // ---- the pi_C Straus term on one wave (latency, not throughput)
+  if (!g_pmc) {
+    G1X* tab;
+    CHK(hipMalloc(&tab, 64 * 32 * sizeof(G1X)));
+    const uint4 ka = {0x89abcdefu, 0x01234567u, 0xdeadbeefu, 0x8badf00du},
+                kb = {0x13579bdfu, 0x2468ace0u, 0x0f1e2d3cu, 0x0a1b2c3du},
+                kc = {0x11111111u, 0x22222222u, 0x33333333u, 0x44444444u},
+                kd = {0x55555555u, 0x66666666u, 0x77777777u, 0x08888888u};
+    const double ms = time_launch([&] { k_straus<<<1, 64>>>(pts, ka, kb, kc, kd, tab, ox); });
+    printf("pi_C Straus term s P + r Q (255-bit scalars, 4-bit windows) on one wave: %.3f ms per launch\n", ms);
+    CHK(hipFree(tab));
   }
   const double base = res[0].gadds;
   printf("%-40s %8s %10s %8s %5s %5s\n", "variant", "ms", "G adds/s", "vs madd", "w/SIMD", "VGPR");

@@ -38,6 +38,10 @@ def main():
         if prof:
             ph = ctx.profile_read()
             span = ph["prove_gpu_span"]["ms"] / steps if "prove_gpu_span" in ph else None
+            if "host_prove_total" in ph:
+                print(f"  host: prove_partial {ph['host_prove_total']['ms'] / steps:.3f} ms, launch "
+                      f"{ph['host_launch']['ms'] / steps:.3f}, finish {ph['host_finish']['ms'] / steps:.3f}, "
+                      f"after last {ph['host_tail_after_last']['ms'] / steps:.3f} ms per proof", flush=True)
             ctx.profile(False)
         return ms, span, p
 

@@ -817,6 +817,8 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   for (int k = 0; k < NUM_SIDE; k++) ZK_HIP(hipStreamSynchronize(ctx->side[k]));
   ZK_HIP(hipStreamSynchronize(st));
   ctx->prof.add_host("host_finish", t_fin);
+  // host wall time of the whole call up to here, against prove_gpu_span
+  ctx->prof.add_host("host_prove_total", ms_since(t_start));
   ctx->prof.collect();
   const uint32_t flags = h_given ? given_flags : *ctx->flags_host.as<uint32_t>();
   p.status = ZK_OK;

@@ -36,6 +36,7 @@ host cores at the full 2^20 size (N = 1), or on all host cores at a bounded
 sample size (N > 1).
 """
 import argparse
+import glob
 import importlib
 import json
 import os
@@ -410,6 +411,12 @@ def traffic_file(name):
         return None, None
 
 
+def latest_profile(suffix):
+    """profiles/rNN_<suffix> of the latest round that has one (None if none)."""
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_{suffix}")))
+    return os.path.basename(found[-1]) if found else suffix
+
+
 def kernel_stats_file(name, prefix):
     """(calls, total ms) of the kernels whose name starts with `prefix` in a
     committed rocprofv3 --stats summary (profiles/<name>, the markdown table
@@ -587,7 +594,7 @@ def ntt_bench(zkp, ctx, log_n, steps, warmup, seed, cpu=True):
     # tools/ntt_only.py at this size (the pass kernels' total over the
     # transforms it ran); the live events above bracket whole calls and
     # include the gaps between the passes' launches
-    ks = kernel_stats_file(f"r03_ntt_2p{log_n}_kernel_stats.md", "k_ntt_pass")
+    ks = kernel_stats_file(latest_profile(f"ntt_2p{log_n}_kernel_stats.md"), "k_ntt_pass")
     if ks:
         kms = ks[1] / (ks[0] / ntt_passes(log_n))
         ksrc = f"rocprofv3 --kernel-trace --stats of tools/ntt_only.py {log_n} ({ks[2]}): {ks[0]} pass launches"

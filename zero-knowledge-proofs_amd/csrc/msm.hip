@@ -371,7 +371,10 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_G2_ATTR k_msm_accum_pair(SegBase
 // G1 row/column sums over lane quads when there are at most this many sums:
 // few sums leave most SIMDs idle, so the 4x lanes are free (single-window
 // G1 MSMs, e.g. H: 512 sums)
-constexpr uint32_t ROWCOL_QUAD_MAX = 600;
+#ifndef ZK_ROWCOL_QUAD_MAX
+#define ZK_ROWCOL_QUAD_MAX 600
+#endif
+constexpr uint32_t ROWCOL_QUAD_MAX = ZK_ROWCOL_QUAD_MAX;
 
 // Buckets whose entries span several accumulate chunks.  A bucket over
 // P = t1 - t0 + 1 chunks is tail(t0) + head(t0+1) + ... + head(t1):

@@ -161,7 +161,8 @@ int zk_ctx_set_schedule(zk_ctx *ctx, int schedule);
  *                         included) is done, so the collectives never queue
  *                         behind a full-occupancy accumulate (for measuring
  *                         one order against the other on one node; no
- *                         effect without a distributed quotient)
+ *                         effect without a distributed quotient or under
+ *                         schedule 3, where everything runs in order)
  * (Test hooks -- the virtual-rank prove, the bare exchange, fault injection
  * -- live in a separate library, include/zkp_test.h.) */
 enum { ZK_OPT_QUOTIENT_PATH = 1, ZK_OPT_PROVE_WIN_C = 2, ZK_OPT_EXCHANGE_TIMEOUT_MS = 3,

@@ -435,6 +435,18 @@ ZK_DI uint32_t pair_swap(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
 }
 ZK_DI uint32_t pair_half() { return threadIdx.x & 1u; }
+// The pair's c0 / c1 on both lanes (DPP quad_perm [0,0,2,2] / [1,1,3,3]):
+// the b operands of the products below, one move each instead of a swap and
+// two per-lane selects (ZK_G2_BCAST=0: A/B build with the swap form)
+#ifndef ZK_G2_BCAST
+#define ZK_G2_BCAST 1
+#endif
+ZK_DI uint32_t pair_even(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xA0, 0xf, 0xf, false);   // quad_perm [0,0,2,2]
+}
+ZK_DI uint32_t pair_odd(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xF5, 0xf, 0xf, false);   // quad_perm [1,1,3,3]
+}
 ZK_DI Fq pair_swap(const Fq& a) {
   Fq o;
 #pragma unroll
@@ -462,10 +474,16 @@ ZK_DI Fq2h f_mul(const Fq2h& a, const Fq2h& b) {
   const uint32_t neg = h ? 0u : ~0u;
 #pragma unroll
   for (int i = 0; i < M; i++) {
-    const uint32_t pa = pair_swap(xa[i]), pb = pair_swap(xb[i]);
+    const uint32_t pa = pair_swap(xa[i]);
     nx1[i] = (int32_t)((pa ^ neg) - neg);
-    y0[i] = h ? pb : xb[i];
-    y1[i] = h ? xb[i] : pb;
+    if constexpr (ZK_G2_BCAST) {   // lane 0: (b0, b1), lane 1: (b0, b1) = (partner, own)
+      y0[i] = pair_even(xb[i]);
+      y1[i] = pair_odd(xb[i]);
+    } else {
+      const uint32_t pb = pair_swap(xb[i]);
+      y0[i] = h ? pb : xb[i];
+      y1[i] = h ? xb[i] : pb;
+    }
   }
   uint32_t m[M], r[M];
   int64_t carry = 0;
@@ -533,15 +551,22 @@ ZK_DI Fq2h f_mul_sub(const Fq2h& a, const Fq2h& b, const Fq2h& c, const Fq2h& d)
   const uint32_t neg = h ? 0u : ~0u;
 #pragma unroll
   for (int i = 0; i < M; i++) {
-    const uint32_t pa = pair_swap(xa[i]), pb = pair_swap(xb[i]);
-    const uint32_t pc = pair_swap(xc[i]), pd = pair_swap(xd[i]);
+    const uint32_t pa = pair_swap(xa[i]), pc = pair_swap(xc[i]);
     na1[i] = (int32_t)((pa ^ neg) - neg);        // lane 0: -a1, lane 1: +a0
     nc0[i] = -(int32_t)xc[i];                    // -c_own
     nc1[i] = (int32_t)((pc ^ ~neg) - ~neg);      // lane 0: +c1, lane 1: -c0
-    y0[i] = h ? pb : xb[i];
-    y1[i] = h ? xb[i] : pb;
-    z0[i] = h ? pd : xd[i];
-    z1[i] = h ? xd[i] : pd;
+    if constexpr (ZK_G2_BCAST) {
+      y0[i] = pair_even(xb[i]);
+      y1[i] = pair_odd(xb[i]);
+      z0[i] = pair_even(xd[i]);
+      z1[i] = pair_odd(xd[i]);
+    } else {
+      const uint32_t pb = pair_swap(xb[i]), pd = pair_swap(xd[i]);
+      y0[i] = h ? pb : xb[i];
+      y1[i] = h ? xb[i] : pb;
+      z0[i] = h ? pd : xd[i];
+      z1[i] = h ? xd[i] : pd;
+    }
   }
   uint32_t m[M], r[M];
   int64_t carry = 0;

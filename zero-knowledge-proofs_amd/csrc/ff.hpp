@@ -516,9 +516,27 @@ ZK_DI Fq2h f_mul(const Fq2h& a, const Fq2h& b) {
   pack28<12, M>(r, o.v);
   return {fp_reduce_once(o)};
 }
+#ifndef ZK_G2_SQR_BCAST
+#define ZK_G2_SQR_BCAST 1
+#endif
 ZK_DI Fq2h f_sqr(const Fq2h& a) {
-  // lane 0: (a0 + a1)(a0 - a1);  lane 1: 2 a1 a0
   const bool h = pair_half();
+  if constexpr (ZK_G2_SQR_BCAST) {
+    // lane 0: (a0 + a1)(a0 - a1);  lane 1: (a0 + a0) a1 -- the doubling moves
+    // into the operand, so no doubled copy and no output select:
+    //   x = partner (lane 0: a1, lane 1: a0), e = a0 on both lanes,
+    //   u = e + x, w = own - (lane 0 ? x : 0)
+    const Fq x = pair_swap(a.v);
+    Fq e, xm;
+    const uint32_t keep = h ? 0u : ~0u;
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      e.v[i] = pair_even(a.v.v[i]);
+      xm.v[i] = x.v[i] & keep;
+    }
+    return {fq_mul(fp_add(e, x), fp_sub(a.v, xm))};
+  }
+  // lane 0: (a0 + a1)(a0 - a1);  lane 1: 2 a1 a0
   const Fq p = pair_swap(a.v);
   const Fq s = fp_add(a.v, p), d = fp_sub(a.v, p);
   Fq u, w;

@@ -157,6 +157,20 @@ ZK_DI void mad_acc_k(uint64_t& acc, uint32_t a, uint32_t b) {
 }
 template <class P>
 constexpr bool mad_chain() { return ZK_MAD_CHAIN && P::NL <= 9; }
+// Two chained v_mad per asm statement: the compiler pads every inline-asm
+// statement with an s_nop (it cannot see inside), so pairs halve the pads
+// (ZK_MAD_PAIR: A/B builds)
+#ifndef ZK_MAD_PAIR
+#define ZK_MAD_PAIR 0
+#endif
+ZK_DI void mad_acc2(uint64_t& acc, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1) {
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0\n\tv_mad_u64_u32 %0, vcc, %3, %4, %0"
+      : "+v"(acc) : "v"(a0), "v"(b0), "v"(a1), "v"(b1) : "vcc");
+}
+ZK_DI void mad_acc2_k(uint64_t& acc, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1) {
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0\n\tv_mad_u64_u32 %0, vcc, %3, %4, %0"
+      : "+v"(acc) : "v"(a0), "s"(b0), "v"(a1), "s"(b1) : "vcc");
+}
 
 template <int N, int M, int LB = 28>
 ZK_DI void unpack28(const uint32_t (&a)[N], uint32_t (&o)[M]) {
@@ -193,15 +207,34 @@ ZK_DI Fp<P> fp_mul_limbs(const uint32_t (&x)[P::NL], const uint32_t (&y)[P::NL])
 #pragma unroll
   for (int k = 0; k < 2 * M - 1; k++) {
     uint64_t acc = carry;
+    if constexpr (mad_chain<P>() && ZK_MAD_PAIR) {
 #pragma unroll
-    for (int i = 0; i < M; i++) {
-      const int j = k - i;
-      if (j >= 0 && j < M) mad_acc<mad_chain<P>()>(acc, x[i], y[j]);
-    }
+      for (int i = 0; i < M; i += 2) {
+        const int j0 = k - i, j1 = k - i - 1;
+        const bool v0 = j0 >= 0 && j0 < M, v1 = i + 1 < M && j1 >= 0 && j1 < M;
+        if (v0 && v1) mad_acc2(acc, x[i], y[j0], x[i + 1], y[j1]);
+        else if (v0) mad_acc<true>(acc, x[i], y[j0]);
+        else if (v1) mad_acc<true>(acc, x[i + 1], y[j1]);
+      }
 #pragma unroll
-    for (int i = 0; i < M; i++) {
-      const int j = k - i;
-      if (i < k && j >= 1 && j < M) mad_acc_k<mad_chain<P>()>(acc, m[i], P::MODL[j]);
+      for (int i = 0; i < M; i += 2) {
+        const int j0 = k - i, j1 = k - i - 1;
+        const bool v0 = i < k && j0 >= 1 && j0 < M, v1 = i + 1 < M && i + 1 < k && j1 >= 1 && j1 < M;
+        if (v0 && v1) mad_acc2_k(acc, m[i], P::MODL[j0], m[i + 1], P::MODL[j1]);
+        else if (v0) mad_acc_k<true>(acc, m[i], P::MODL[j0]);
+        else if (v1) mad_acc_k<true>(acc, m[i + 1], P::MODL[j1]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < M; i++) {
+        const int j = k - i;
+        if (j >= 0 && j < M) mad_acc<mad_chain<P>()>(acc, x[i], y[j]);
+      }
+#pragma unroll
+      for (int i = 0; i < M; i++) {
+        const int j = k - i;
+        if (i < k && j >= 1 && j < M) mad_acc_k<mad_chain<P>()>(acc, m[i], P::MODL[j]);
+      }
     }
     if (k < M) {
       m[k] = ((uint32_t)acc * P::INVL) & MASK;

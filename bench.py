@@ -4,6 +4,7 @@ configs[4] on N > 1), plus G1 MSM scalar-point pairs/s at 2^20 (configs[1])
 and the 2^22 Fr NTT (configs[2]) on rank 0 of a one-GPU run.
 
   python bench.py [--gpus 1] [--steps K] [--warmup W]
+  python bench.py --gpus N ...          (starts its own N rank processes)
   torchrun --nproc-per-node N bench.py --gpus N ...
 
 A step = one full prove (quotient NTTs + 5 MSMs + host tail) with the proving
@@ -29,6 +30,20 @@ key and the witness already resident in HBM.
          waiting for the distributed quotient) and `cpu_baseline` (the oracle on
          a bounded sample, rank 0).  --scaling weak keeps 2^log_n constraints
          per GPU instead.
+
+Without a launcher (`--gpus N`, no WORLD_SIZE in the environment) the
+parent process starts the N ranks itself as fresh child processes (RANK /
+LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set), before
+importing torch or the package: it never touches a GPU, the children share
+its stdout (rank 0's JSON line), and it exits non-zero if any rank fails.
+
+The ranks' control plane (barriers, the max-over-ranks timing, agreements) is
+a gloo group; the library's RCCL communicator (the distributed quotient's
+all-to-alls) and a torch RCCL group (the partials' all-gather) are attached
+after it.  If either fails on any rank -- or the first distributed proof
+does -- every rank carries on without it, labelled in the line ("quotient":
+"replicated (rccl: ...)", "partials_gather": "gloo (rccl: ...)"), so the
+MSM-scaling curve still comes out.
 
 Rank 0 prints one JSON line.  The CPU baseline leg times the C restatement
 (oracle/, test infrastructure) single-threaded on a bounded sample and on all
@@ -218,6 +233,21 @@ def oracle_leg(fn, threads):
         oracle.set_threads(prev)
 
 
+CORES_NOTE = ("the lease's CPU share: the GPU box shows every CPU of the shared host in its affinity set and sets "
+              "OMP_NUM_THREADS to one GPU's share, which this leg keeps (the box rules forbid sizing worker pools "
+              "beyond it); `all_affinity_cpus_projection` scales the measured 1-thread rate to every affinity CPU")
+
+
+def affinity_projection(v1, v_nt, nt):
+    """The oracle on EVERY CPU of the affinity set, projected linearly from
+    its measured 1-thread rate: an upper bound (the measured nt-thread rate
+    shows the real efficiency), so GPU / projection is a lower bound on the
+    GPU's lead over this host."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return {"cpus": aff, "value": round(v1 * aff, 1), "basis": "1-thread rate x affinity CPUs (linear upper bound)",
+            "measured_efficiency_at_lease_threads": round(v_nt / (v1 * nt), 3) if nt > 1 else None}
+
+
 def host_cpu():
     model = platform.processor() or ""
     try:
@@ -285,7 +315,10 @@ def cpu_baseline(zkp, ctx, n, params, r, s, z_host, gpu_proof, log_n_1t, seed):
     dpk1.free()
     cpu = host_cpu()
     lab = host_threads_label(nt)
+    v1 = n1 / dt_1
     return {"value": round(n / dt_all, 2), "unit": "constraints/s", "cores": nt, "kind": "port",
+            "cores_note": CORES_NOTE,
+            "all_affinity_cpus_projection": affinity_projection(v1, n / dt_all, nt),
             "sample": f"oracle/zk_oracle.c prove() of the full 2^{n.bit_length() - 1}-constraint circuit on "
                       f"{lab['label']} (OpenMP: MSM point chunks, FFT butterflies), {dt_all:.2f} s, same pk/z/r/s "
                       f"as the GPU's timed proof",
@@ -323,7 +356,19 @@ def cpu_sample_baseline(zkp, ctx, log_n, params, r, s, seed):
     if rc != 0:
         raise RuntimeError(f"oracle prove failed: {rc}")
     lab = host_threads_label(nt)
+    # the 1-thread rate on a 2^15 sample for the all-CPU projection
+    n1 = 1 << 15
+    csr1 = oracle.CSR.synthetic(n1)
+    crs1 = zkp.CRS.generate_from_qap(ctx, zkp.QAP(zkp.CSRMatrices.synthetic(n1)), zkp.SetupParams(*params), 1)
+    opk1 = oracle_pk(oracle, crs1.pk)
+    z1 = ctx.synthetic_witness(n1, seed).cpu().numpy().view(np.uint64)
+    oracle.set_threads(1)
+    t0 = time.perf_counter()
+    oracle.prove(opk1, csr1, z1, 1, r, s)
+    v1 = n1 / (time.perf_counter() - t0)
+    oracle.set_threads(nt)
     return {"value": round(n / dt, 2), "unit": "constraints/s", "cores": nt, "kind": "port",
+            "cores_note": CORES_NOTE, "all_affinity_cpus_projection": affinity_projection(v1, n / dt, nt),
             "sample": f"oracle/zk_oracle.c prove() of a 2^{log_n}-constraint sample of the same synthetic circuit "
                       f"family on {lab['label']} (rank 0, after the timed region), {dt:.2f} s; the oracle's "
                       f"constraints/s barely depends on size (2^20 vs 2^24 within 10 %, DESIGN.md 4)",
@@ -363,9 +408,11 @@ def anchor_bench(zkp, ctx, log_n, params, r, s, seed, steps, warmup, win_c=0):
         ctx.set_schedule(3)
         ctx.profile(True)
         ks = max(2, steps // 2)
+        t0 = time.perf_counter()
         for _ in range(ks):
             p3 = run()
         torch.cuda.synchronize()
+        t_ser = (time.perf_counter() - t0) / ks
         prof = ctx.profile_read()
         ctx.profile(False)
         ctx.set_schedule(0)
@@ -385,6 +432,10 @@ def anchor_bench(zkp, ctx, log_n, params, r, s, seed, steps, warmup, win_c=0):
                          "g1_pairs": g1, "g2_pairs": g2,
                          "timing": "HIP events around every MSM kernel (sort, accumulate, merge, bucket sums) of "
                                    "serial-schedule proves (zk_ctx_set_schedule 3), per proof"},
+            "serial_schedule": {"ms_per_step": round(t_ser * 1e3, 3), "steps": ks,
+                                "phases_ms_total": phase_table(prof),
+                                "note": "every kernel in order on one stream, HIP events per phase; totals over "
+                                        "`steps` proofs"},
             "window_bits": win_c or (22 if n >= 1 << 24 else 16),
             "roofline": roofline_from(prof, log_n) if not win_c else None,
             "proof_compressed": hexp,
@@ -642,6 +693,63 @@ def ntt_bench(zkp, ctx, log_n, steps, warmup, seed, cpu=True):
     return rec
 
 
+def spawn_ranks(n):
+    """`--gpus N` without torchrun: start the N ranks as fresh child processes
+    (this process has not imported torch or the package and never touches a
+    GPU), wait for them, and return the job's exit code -- the first non-zero
+    rank code; ranks still running 60 s after a rank failed are killed (by
+    their own PIDs)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for rank in range(n):
+        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env))
+
+    def forward(sig, _frame):
+        for pr in procs:
+            if pr.poll() is None:
+                pr.send_signal(sig)
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
+    t_fail = None
+    while True:
+        codes = [pr.poll() for pr in procs]
+        if all(c is not None for c in codes):
+            break
+        if t_fail is None and any(c not in (None, 0) for c in codes):
+            t_fail = time.time()
+            log(f"[bench] a rank failed (exit codes {codes}); waiting 60 s for the others")
+        if t_fail is not None and time.time() - t_fail > 60:
+            for pr in procs:
+                if pr.poll() is None:
+                    pr.kill()
+        time.sleep(0.2)
+    bad = [c for c in codes if c != 0]
+    if not bad:
+        return 0
+    return bad[0] if bad[0] > 0 else 128 - bad[0]
+
+
+def probe(dist, fn):
+    """Run fn() on every rank and agree on the outcome over the (gloo) control
+    group: (result, None) if it succeeded everywhere, else (result or None,
+    "rank k: <error>") of the first failing rank -- the same on every rank."""
+    try:
+        out, err = fn(), None
+    except Exception as e:   # noqa: BLE001 -- reported, and every rank follows the same branch
+        out, err = None, f"{type(e).__name__}: {e}"[:300]
+    errs = [None] * dist.get_world_size()
+    dist.all_gather_object(errs, err)
+    bad = [(k, e) for k, e in enumerate(errs) if e]
+    return out, (f"rank {bad[0][0]}: {bad[0][1]}" if bad else None)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -665,6 +773,13 @@ def main():
     ap.add_argument("--schedule", type=int, choices=(0, 3), default=0,
                     help="prove stream schedule of the timed region (3: every kernel serial, for profilers)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    if os.environ.get("ZK_BENCH_LAUNCH_ECHO"):   # CPU test of the launcher: no torch, no GPU
+        sys.stdout.write(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE",
+                                                                      "MASTER_ADDR")}) + "\n")
+        sys.stdout.flush()
+        sys.exit(int(os.environ["ZK_BENCH_LAUNCH_ECHO"]) if os.environ.get("RANK") == "1" else 0)
 
     import torch
     zkp = importlib.import_module("zero-knowledge-proofs_amd")
@@ -674,38 +789,75 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # Rehearsal knobs (not the bench contract): ZK_BENCH_DIST_BACKEND=gloo and
-    # ZK_BENCH_DEVICE=0 run N ranks on one GPU with CPU-side collectives: the
-    # distributed quotient's all-to-alls then go through the library's
+    # ZK_BENCH_DEVICE=0 run N ranks on one GPU with CPU-side collectives only:
+    # the distributed quotient's all-to-alls then go through the library's
     # host-staged exchange over the gloo group ("quotient":
-    # "distributed-host") instead of RCCL.
+    # "distributed-host") instead of RCCL.  ZK_BENCH_FAIL_RCCL=k makes rank
+    # k's RCCL attach fail (tests of the fallback below).
     backend = os.environ.get("ZK_BENCH_DIST_BACKEND", "nccl")
     local = int(os.environ.get("ZK_BENCH_DEVICE", local))
+    fail_rccl = int(os.environ.get("ZK_BENCH_FAIL_RCCL", "-1"))
     torch.cuda.set_device(local)
     dist = None
+    coll_dev = "cpu"   # control-plane tensors (gloo)
     if world > 1:
         import torch.distributed as dist
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-        else:
-            dist.init_process_group(backend)
-    coll_dev = f"cuda:{local}" if backend == "nccl" else "cpu"
+        from datetime import timedelta
+        dist.init_process_group("gloo", timeout=timedelta(seconds=900))
 
     ctx = zkp.Context(local)
     quotient_mode = "local"
+    data_group, gather_mode = None, None
     if dist:
-        quotient_mode = "replicated"
-        if backend == "nccl":
+        quotient_mode, gather_mode = "replicated", "gloo"
+        if backend == "nccl" or fail_rccl >= 0:
             # one RCCL communicator inside the library for the distributed
             # quotient (three all-to-alls per proof over xGMI); the unique id
-            # travels over the torch process group.  A failed attach is fatal:
-            # a replicated quotient would be a different (slower) workload.
-            obj = [zkp.Context.rccl_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0)
-            ctx.attach_rccl(obj[0], rank, world)
-            quotient_mode = "distributed-rccl"
+            # travels over the control group.  If the attach fails on any
+            # rank, every rank detaches and proves with the replicated
+            # quotient, labelled as such.
+            def attach():
+                uid, err = None, None
+                if rank == 0:
+                    try:
+                        uid = zkp.Context.rccl_unique_id()
+                    except Exception as e:   # noqa: BLE001 -- broadcast, then raised on every rank
+                        err = str(e)
+                obj = [(uid, err)]
+                dist.broadcast_object_list(obj, src=0)
+                if obj[0][1]:
+                    raise zkp.ExchangeError(f"rank 0 rccl_unique_id: {obj[0][1]}")
+                if fail_rccl >= 0:   # rehearsal: rank fail_rccl fails, the others skip the attach
+                    if rank == fail_rccl:
+                        raise zkp.ExchangeError("ZK_BENCH_FAIL_RCCL: attach failure injected")
+                    return
+                ctx.attach_rccl(obj[0][0], rank, world)
+            _, err = probe(dist, attach)
+            if err:
+                ctx.detach_exchange()
+                quotient_mode = f"replicated (rccl: {err})"
+                log(f"[bench] RCCL attach failed ({err}): replicated quotient")
+            else:
+                quotient_mode = "distributed-rccl"
         else:
             ctx.attach_exchange(zkp.TorchExchange(), rank, world)
             quotient_mode = "distributed-host"
+        if backend == "nccl":
+            # the partials' all-gather over RCCL (a torch nccl group beside
+            # the gloo control plane), gloo if that group does not come up
+            def rccl_group():
+                g = dist.new_group(backend="nccl")
+                t = torch.zeros(world, dtype=torch.int64, device=f"cuda:{local}")
+                dist.all_gather_into_tensor(t, torch.full((1,), rank, dtype=torch.int64, device=t.device), group=g)
+                if t.cpu().tolist() != list(range(world)):
+                    raise RuntimeError(f"rccl all-gather check failed: {t.cpu().tolist()}")
+                return g
+            data_group, err = probe(dist, rccl_group)
+            if err:
+                data_group, gather_mode = None, f"gloo (rccl: {err})"
+                log(f"[bench] RCCL group failed ({err}): partials over gloo")
+            else:
+                gather_mode = "rccl"
     strong = world > 1 and args.scaling == "strong"
     if world == 1:
         n = 1 << args.log_n
@@ -731,14 +883,42 @@ def main():
     zlen = 3 * n + 1
     log(f"[bench] setup {t_setup:.2f}s; witness ready ({zlen} vars)")
 
+    def gather(part):
+        """The ONE exchange of the MSM shards: every rank's 1.5 KB partials,
+        all-gathered (RCCL when its group came up, else gloo)."""
+        if data_group is not None:
+            mine = torch.frombuffer(bytearray(part), dtype=torch.uint8).to(f"cuda:{local}")
+            allp = torch.empty(world * len(part), dtype=torch.uint8, device=mine.device)
+            dist.all_gather_into_tensor(allp, mine, group=data_group)
+        else:
+            mine = torch.frombuffer(bytearray(part), dtype=torch.uint8)
+            allp = torch.empty(world * len(part), dtype=torch.uint8)
+            dist.all_gather_into_tensor(allp, mine)
+        b = allp.cpu().numpy().tobytes()
+        return [b[k * len(part):(k + 1) * len(part)] for k in range(world)]
+
     def step():
         if world == 1:
             return zkp.Prover.prove_device(dpk, d_z.data_ptr(), zlen, 1, r, s)
         part = zkp.Prover.prove_partial(dpk, d_z.data_ptr(), zlen, 1, r, s)
-        mine = torch.frombuffer(bytearray(part), dtype=torch.uint8).to(coll_dev)
-        bufs = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(bufs, mine)                      # the one RCCL exchange
-        return zkp.Prover.combine([b.cpu().numpy().tobytes() for b in bufs], r, s)
+        return zkp.Prover.combine(gather(part), r, s)
+
+    if dist:
+        # the first sharded proof, agreed: a distributed quotient that fails
+        # on any rank (RCCL between real peers) -> every rank detaches and
+        # carries on with the replicated quotient, labelled
+        _, err = probe(dist, lambda: zkp.Prover.prove_partial(dpk, d_z.data_ptr(), zlen, 1, r, s))
+        if err and quotient_mode.startswith("distributed"):
+            ctx.detach_exchange()
+            quotient_mode = f"replicated ({quotient_mode.split('-')[1]}: first distributed proof failed: {err})"
+            log(f"[bench] first distributed proof failed ({err}): replicated quotient")
+            _, err = probe(dist, lambda: zkp.Prover.prove_partial(dpk, d_z.data_ptr(), zlen, 1, r, s))
+        if err:
+            raise SystemExit(f"sharded prove failed: {err}")
+        if data_group is not None:
+            _, err = probe(dist, lambda: gather(b"\0" * zkp.PARTIAL_BYTES))
+            if err:
+                data_group, gather_mode = None, f"gloo (rccl all-gather failed: {err})"
 
     ctx.set_schedule(args.schedule)
     for _ in range(args.warmup):
@@ -785,10 +965,7 @@ def main():
 
         def step_host():
             part = zkp.Prover.prove_partial_host(dpk, z_slice, zlen, 1, r, s)
-            mine = torch.frombuffer(bytearray(part), dtype=torch.uint8).to(coll_dev)
-            bufs = [torch.empty_like(mine) for _ in range(world)]
-            dist.all_gather(bufs, mine)
-            return zkp.Prover.combine([b.cpu().numpy().tobytes() for b in bufs], r, s)
+            return zkp.Prover.combine(gather(part), r, s)
         step_host()
         dist.barrier()
         t0 = time.perf_counter()
@@ -942,7 +1119,7 @@ def main():
                 c16 = anchor_bench(zkp, ctx, args.anchor_log_n, params, r, s, args.seed, max(2, args.steps // 2),
                                    1, win_c=16)
                 anc["same_plan_c16"] = {k: c16[k] for k in ("ms_per_step", "value", "msm_only", "window_bits",
-                                                            "bit_exact_vs_oracle")}
+                                                            "bit_exact_vs_oracle", "serial_schedule")}
             extra["strong_scaling_anchor"] = anc
     if rank == 0:
         if world == 1:
@@ -962,7 +1139,10 @@ def main():
                        "constraints": n, "constraints_per_gpu": n // world, "num_public": 1,
                        "parallelism": (f"msm-shard{world}+quotient-a2a" if quotient_mode == "distributed-rccl"
                                        else f"msm-shard{world}" if world > 1 else "single-gpu"),
-                       "quotient": quotient_mode, "setup_s": round(t_setup, 2)},
+                       "quotient": quotient_mode, "setup_s": round(t_setup, 2),
+                       **({"partials_gather": gather_mode,
+                           "launcher": "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ else "bench.py"}
+                          if world > 1 else {})},
             "msm_pairs_per_s": {"g1": round(g1_pairs / (ms_step / 1e3), 1), "g2": round(g2_pairs / (ms_step / 1e3), 1),
                                 "total": round((g1_pairs + g2_pairs) / (ms_step / 1e3), 1),
                                 "note": "scalar-point pairs of the reference's 5 MSMs per proof (G1 10n+6, G2 3n+3) "
@@ -974,9 +1154,13 @@ def main():
         }
         rec.update(extra)
         rec.setdefault("cpu_baseline", None)
+        proj = (rec["cpu_baseline"] or {}).get("all_affinity_cpus_projection")
+        if proj:
+            proj["gpu_over_projection"] = round(rec["value"] / proj["value"], 2)
         if world > 1 and log_n_total == 24 and args.seed == DEFAULT_SEED:
             rec["bit_exact_vs_oracle"] = rec["proof_compressed"] == ORACLE_2P24   # the pinned oracle proof
-        print(json.dumps(rec), flush=True)
+        sys.stdout.write(json.dumps(rec) + "\n")   # one write: ranks share the launcher's stdout
+        sys.stdout.flush()
     ctx.close()
     if dist:
         dist.destroy_process_group()

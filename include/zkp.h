@@ -308,6 +308,9 @@ int zk_groth16_prove_combine(const zk_prove_partial *parts, size_t nparts,
  * (shard, nshards) and nshards is 2, 4 or 8; otherwise every rank computes
  * the whole quotient.  No reference counterpart (multi-GPU). */
 int zk_rccl_unique_id(uint8_t out[128]);   /* one rank makes it, all attach with it */
+/* The communicator is created non-blocking and polled under the ctx's
+ * exchange watchdog (ZK_OPT_EXCHANGE_TIMEOUT_MS): a peer that never attaches
+ * makes this return ZK_ERR_RCCL after the timeout instead of hanging. */
 int zk_ctx_attach_rccl(zk_ctx *ctx, const uint8_t unique_id[128], int rank, int world);
 /* The same distributed quotient over a host-staged exchange: each of the
  * three all-to-alls brings this rank's world chunks of chunk_bytes (chunk k
@@ -327,6 +330,12 @@ typedef struct {
   void *user;
 } zk_exchange_ops;
 int zk_ctx_attach_exchange(zk_ctx *ctx, const zk_exchange_ops *ops, int rank, int world);
+/* Drop the ctx's exchange (RCCL: ncclCommAbort, local -- every rank is
+ * expected to detach too); later proofs of sharded keys compute the whole
+ * quotient on every rank.  A caller whose attach or first distributed proof
+ * failed on some rank detaches everywhere and carries on replicated.  No-op
+ * without an exchange.  No reference counterpart. */
+int zk_ctx_detach_exchange(zk_ctx *ctx);
 /* ---------------------------------------------------------------- QAP --- */
 /* QAP::evaluate_at (crates/groth16-qap/src/lib.rs:190-220): out[0..2] =
  * A(point), B(point), C(point) = sum_i z_i A_i(point) etc., out[3] = Z(point)

@@ -22,7 +22,11 @@ the 8-GPU run takes (only ncclAllToAll itself differs).
     gives the same partial as the distributed quotient, and so does
     ZK_OPT_EXCHANGE_FIRST = 1 (the MSMs waiting for the quotient);
   * a non-canonical value in a variable no row references (so no stage reads
-    it) is still rejected by the rank var_owner gives it."""
+    it) is still rejected by the rank var_owner gives it -- and, the ranks'
+    witness flags being agreed, by every rank;
+  * ZK_OPT_DIST_QUOTIENT set differently on the ranks fails every rank with
+    ZK_ERR_ARG (the mode agreement); after zk_ctx_detach_exchange every rank
+    proves with the replicated quotient."""
 import json
 import os
 import socket
@@ -99,6 +103,18 @@ def _worker(rank, world, port, log_n, seed, out_dir, mode):
         res["exchange_first_equal"] = (zkp.Prover.prove_partial_host(dpk, zs, len(z), 1, r, s) == part and
                                        zkp.Prover.prove_partial(dpk, dz.data_ptr(), len(z), 1, r, s) == part)
         ctx.set_option(zkp.ZK_OPT_EXCHANGE_FIRST, 0)
+        # ZK_OPT_DIST_QUOTIENT set on rank 1 only: the mode agreement fails
+        # the proof on BOTH ranks (ZK_ERR_ARG) instead of rank 0 entering the
+        # all-to-alls alone; the exchange stays usable
+        if rank == 1:
+            ctx.set_option(zkp.ZK_OPT_DIST_QUOTIENT, 0)
+        try:
+            zkp.Prover.prove_partial(dpk, dz.data_ptr(), len(z), 1, r, s)
+            res["mode_mismatch_error"] = None
+        except Exception as e:   # noqa: BLE001 -- the kind is the result
+            res["mode_mismatch_error"] = type(e).__name__
+        ctx.set_option(zkp.ZK_OPT_DIST_QUOTIENT, -1)
+        res["after_mismatch_equal"] = zkp.Prover.prove_partial(dpk, dz.data_ptr(), len(z), 1, r, s) == part
         # one extra variable that no row references, holding r (non-canonical)
         csr = zkp.CSRMatrices.synthetic(n)
         qx = zkp.QAP(zkp.CSRMatrices(n, 3 * n + 2, csr.mats))
@@ -111,6 +127,10 @@ def _worker(rank, world, port, log_n, seed, out_dir, mode):
         except Exception as e:   # noqa: BLE001
             res["extra_error"] = type(e).__name__
         dx.free()
+        # detached on every rank: the replicated quotient, same partial
+        ctx.detach_exchange()
+        res["detached_ranges"] = [[int(a), int(b)] for a, b in dpk.witness_ranges()]
+        res["detached_equal"] = zkp.Prover.prove_partial_host(dpk, dpk.witness_slice(z), len(z), 1, r, s) == part
     if mode == "fault":
         if rank == 1:
             ctx.test_fault_after_exchange(2)
@@ -189,6 +209,12 @@ def test_slice_errors_replicated_quotient_exchange_first_and_unreferenced_variab
         assert r["after_short_equal"], r                       # the exchange survived
         assert r["replicated_ranges"] == [[0, zlen]] and r["replicated_equal"], r
         assert r["exchange_first_equal"], r
-    # var_owner gives the unreferenced variable (index 3n+1 of 3n+2) to rank 1
+        assert r["mode_mismatch_error"] == "ValueError", r    # both ranks, through the mode agreement
+        assert r["after_mismatch_equal"], r
+        assert r["detached_ranges"] == [[0, zlen]] and r["detached_equal"], r
+    # var_owner gives the unreferenced variable (index 3n+1 of 3n+2) to rank 1,
+    # which finds it >= r; the flag words are agreed, so rank 0 -- whose own
+    # checks pass -- fails with it (an SPMD caller gathering partials next
+    # never waits for a rank that raised)
     assert res[1]["extra_in_ranges"] and res[1]["extra_error"] == "ValueError", res[1]
-    assert not res[0]["extra_in_ranges"] and res[0]["extra_error"] is None, res[0]
+    assert not res[0]["extra_in_ranges"] and res[0]["extra_error"] == "ValueError", res[0]

@@ -1,5 +1,7 @@
 """Groth16 prove / setup on the GPU: bit-exact against the golden fixtures
 (independent literal restatement) and the C oracle (same pk, z, r, s)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -158,6 +160,43 @@ def test_rccl_attach_single_rank(zkp):
         c.attach_rccl(uid, 0, 1)
         for chunk, status in ((1, 0), (37, 5), (3 << 20, -2), (96 << 20, 7)):
             assert c.test_exchange(chunk, status) == status
+        c.attach_rccl(zkp.Context.rccl_unique_id(), 0, 1)   # re-attach replaces it
+        assert c.test_exchange(64, 3) == 3
+        c.detach_exchange()
+        c.detach_exchange()                                   # no-op
+        with pytest.raises(ValueError):
+            c.test_exchange(64, 0)                            # nothing attached
+
+
+_MISSING_PEER = r"""
+import importlib, sys, time
+sys.path.insert(0, sys.argv[1])
+zkp = importlib.import_module("zero-knowledge-proofs_amd")
+with zkp.Context(0) as c:
+    c.set_option(zkp.ZK_OPT_EXCHANGE_TIMEOUT_MS, 3000)
+    t = time.perf_counter()
+    try:
+        c.attach_rccl(zkp.Context.rccl_unique_id(), 0, 2)
+        print("ATTACHED")
+    except zkp.ExchangeError as e:
+        print("EXCHANGE_ERROR %.1f" % (time.perf_counter() - t))
+"""
+
+
+@pytest.mark.timeout(120)
+def test_rccl_attach_missing_peer_times_out(zkp):
+    """Rank 0 of a world-2 communicator whose rank 1 never attaches: the
+    non-blocking ncclCommInitRankConfig is polled under the exchange watchdog,
+    so the attach fails with ZK_ERR_RCCL after the timeout instead of waiting
+    forever (bench.py's N > 1 path then carries on with the replicated
+    quotient).  In a child process with its own time limit."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = subprocess.run([sys.executable, "-c", _MISSING_PEER, root], capture_output=True, text=True, timeout=100)
+    out = res.stdout.strip().splitlines()
+    assert res.returncode == 0 and out and out[-1].startswith("EXCHANGE_ERROR"), (res.stdout, res.stderr[-2000:])
+    assert float(out[-1].split()[1]) < 30
 
 
 def test_prove_all_ones_witness(ctx, zkp, oracle):

@@ -69,19 +69,33 @@ int main() {
   if (pairing_product_is_one(ps, qs)) return 6;
   (void)qx0;
   (void)qy0;
-  // divstep inversion == Fermat, on 0, 1, m - 1 and 2000 pseudo-random values
+  // divstep inversion == Fermat, on 0, 1, -1, the raw residues m - 1, m - 2,
+  // 2^380, 2^380 - 1 (top-limb sign / carry boundaries of the signed limbs)
+  // and 2000 residues uniform in [0, m) (381-bit rejection sampling)
   {
     uint64_t st = 0x9e3779b97f4a7c15ull;
-    for (int k = 0; k < 2003; k++) {
+    auto raw = [](uint64_t sub) {   // m - sub
+      Fq a;
+      std::memcpy(a.l, FQ_M, 48);
+      a.l[0] -= sub;
+      return a;
+    };
+    for (int k = 0; k < 2007; k++) {
       Fq a = zero();
       if (k == 1) a = one();
       else if (k == 2) a = neg(one());
-      else if (k > 2) {
-        for (int i = 0; i < 6; i++) {
-          st ^= st << 13; st ^= st >> 7; st ^= st << 17;
-          a.l[i] = st;
-        }
-        a.l[5] &= 0x0fffffffffffffffull;   // < 2^380 < m
+      else if (k == 3) a = raw(1);
+      else if (k == 4) a = raw(2);
+      else if (k == 5) a.l[5] = 1ull << 60;                       // 2^380
+      else if (k == 6) { for (int i = 0; i < 5; i++) a.l[i] = ~0ull; a.l[5] = (1ull << 60) - 1; }
+      else if (k > 6) {
+        do {
+          for (int i = 0; i < 6; i++) {
+            st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+            a.l[i] = st;
+          }
+          a.l[5] &= 0x1fffffffffffffffull;   // 381 bits, then reject >= m
+        } while (geq_m(a.l));
       }
       const Fq x = inv(a), y = inv_fermat(a);
       if (std::memcmp(&x, &y, sizeof x) != 0) return 7;

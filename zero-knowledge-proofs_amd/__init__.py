@@ -52,6 +52,7 @@ EXPORTS = (
     "zk_msm_g2_upload_windows", "zk_build_id", "zk_ctx_set_schedule", "zk_qap_evaluate_at",
     "zk_poly_evaluate_batch", "zk_synthetic_witness_dev", "zk_ctx_set_option", "zk_ctx_timeline_read",
     "zk_ctx_attach_exchange", "zk_groth16_witness_ranges", "zk_groth16_prove_partial_host",
+    "zk_ctx_detach_exchange",
 )
 # include/zkp_test.h (libzkp_amd_test.so)
 TEST_EXPORTS = ("zk_test_prove_virtual_shards", "zk_test_exchange", "zk_test_fault_after_exchange",
@@ -316,6 +317,13 @@ class Context:
         buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
         _check(lib().zk_ctx_attach_rccl(C.c_void_p(self._h), buf, C.c_int(rank), C.c_int(world)), self,
                "zk_ctx_attach_rccl")
+
+    def detach_exchange(self):
+        """zk_ctx_detach_exchange: drop the attached exchange (RCCL: a local
+        ncclCommAbort); sharded keys then compute the whole quotient on every
+        rank.  Every rank of the job detaches together."""
+        _check(lib().zk_ctx_detach_exchange(C.c_void_p(self._h)), self, "zk_ctx_detach_exchange")
+        self._exchange_refs = None
 
     def test_exchange(self, chunk_bytes, status):
         """zk_test_exchange: one all-to-all and one status agreement on the

@@ -523,8 +523,20 @@ int zk_rccl_unique_id(uint8_t out[128]) {
 int zk_ctx_attach_rccl(zk_ctx* ctx, const uint8_t unique_id[128], int rank, int world) {
   if (!ctx || !unique_id || world < 1 || rank < 0 || rank >= world) return ZK_ERR_ARG;
   ZK_GUARD(ctx, {
-    ctx->exch = make_rccl_exchange(unique_id, rank, world);
-    ctx->exch->timeout_ms = ctx->exch_timeout_ms;
+    ctx->exch.reset();
+    ctx->exch = make_rccl_exchange(unique_id, rank, world, ctx->exch_timeout_ms);
+    return ZK_OK;
+  })
+}
+
+int zk_ctx_detach_exchange(zk_ctx* ctx) {
+  if (!ctx) return ZK_ERR_ARG;
+  ZK_GUARD(ctx, {
+    if (ctx->exch) {
+      ZK_HIP(hipStreamSynchronize(ctx->stream));
+      ctx->exch->abort();   // local: the peers detach too, nobody waits for a collective
+      ctx->exch.reset();
+    }
     return ZK_OK;
   })
 }
@@ -533,6 +545,7 @@ int zk_ctx_attach_exchange(zk_ctx* ctx, const zk_exchange_ops* ops, int rank, in
   if (!ctx || !ops || !ops->all_to_all || !ops->all_reduce_max || world < 1 || rank < 0 || rank >= world)
     return ZK_ERR_ARG;
   ZK_GUARD(ctx, {
+    ctx->exch.reset();
     ctx->exch = make_host_exchange(*ops, rank, world);
     ctx->exch->timeout_ms = ctx->exch_timeout_ms;
     return ZK_OK;

@@ -305,10 +305,33 @@ void sync_watchdog(hipStream_t st, Exchange& ex) {
 }
 
 // --------------------------------------------------------------- RCCL ---
-#define ZK_NCCL(call)                                                                          \
+// The communicator is created non-blocking (ncclConfig_t::blocking = 0):
+// ncclCommInitRankConfig and the collectives may return ncclInProgress, and
+// the operation then completes in the background; nccl_wait polls
+// ncclCommGetAsyncError until it has, under the exchange's watchdog.  A
+// blocking ncclCommInitRank waits forever for a peer that never calls it
+// (a rank that failed before the attach), which no caller can recover from.
+static void nccl_wait(ncclComm_t comm, double timeout_ms, const char* what) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    ncclResult_t st = ncclInProgress;
+    const ncclResult_t q = ncclCommGetAsyncError(comm, &st);
+    if (q != ncclSuccess) throw Error(ZK_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(q));
+    if (st == ncclSuccess) return;
+    if (st != ncclInProgress) throw Error(ZK_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(st));
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (ms > timeout_ms)
+      throw Error(ZK_ERR_RCCL, std::string(what) + ": not complete within the exchange timeout (a peer missing?)");
+    std::this_thread::yield();
+  }
+}
+
+#define ZK_NCCL(comm, timeout_ms, call)                                                        \
   do {                                                                                         \
-    ncclResult_t r_ = (call);                                                                  \
-    if (r_ != ncclSuccess)                                                                     \
+    const ncclResult_t r_ = (call);                                                            \
+    if (r_ == ncclInProgress)                                                                  \
+      nccl_wait((comm), (timeout_ms), #call);                                                  \
+    else if (r_ != ncclSuccess)                                                                \
       throw ::zk::Error(ZK_ERR_RCCL, std::string(#call) + ": " + ncclGetErrorString(r_));     \
   } while (0)
 
@@ -317,17 +340,26 @@ struct RcclExchange : Exchange {
   DevBuf stat;
   PinnedBuf stat_host;
   void all_to_all(const void* send, void* recv, size_t chunk_bytes, hipStream_t st) override {
-    ZK_NCCL(ncclAllToAll(send, recv, chunk_bytes, ncclUint8, comm, st));
+    ZK_NCCL(comm, timeout_ms, ncclAllToAll(send, recv, chunk_bytes, ncclUint8, comm, st));
   }
   int agree_max(int status, hipStream_t st) override {
+    int32_t v[2] = {status, 0};
+    agree_max2(v, st);
+    return v[0];
+  }
+  void agree_max2(int32_t v[2], hipStream_t st) override {
     stat.ensure(16);
     stat_host.ensure(16);
-    *stat_host.as<int32_t>() = status;
-    ZK_HIP(hipMemcpyAsync(stat.p, stat_host.p, 4, hipMemcpyHostToDevice, st));
-    ZK_NCCL(ncclAllReduce(stat.p, stat.p, 1, ncclInt32, ncclMax, comm, st));
-    ZK_HIP(hipMemcpyAsync(stat_host.p, stat.p, 4, hipMemcpyDeviceToHost, st));
+    std::memcpy(stat_host.p, v, 8);
+    ZK_HIP(hipMemcpyAsync(stat.p, stat_host.p, 8, hipMemcpyHostToDevice, st));
+    ZK_NCCL(comm, timeout_ms, ncclAllReduce(stat.p, stat.p, 2, ncclInt32, ncclMax, comm, st));
+    ZK_HIP(hipMemcpyAsync(stat_host.p, stat.p, 8, hipMemcpyDeviceToHost, st));
     sync_watchdog(st, *this);
-    return *stat_host.as<int32_t>();
+    std::memcpy(v, stat_host.p, 8);
+  }
+  bool agree_max_dev(uint32_t* d_val, hipStream_t st) override {
+    ZK_NCCL(comm, timeout_ms, ncclAllReduce(d_val, d_val, 1, ncclUint32, ncclMax, comm, st));
+    return true;
   }
   // ncclCommAbort sets the communicator's abort flag, which its in-flight
   // kernels poll: this rank's collectives end, and so do the peers' once
@@ -390,17 +422,32 @@ static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
 
 void rccl_unique_id(uint8_t out[128]) {
   ncclUniqueId id;
-  ZK_NCCL(ncclGetUniqueId(&id));
+  const ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) throw Error(ZK_ERR_RCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
   std::memcpy(out, &id, 128);
 }
 
-std::unique_ptr<Exchange> make_rccl_exchange(const uint8_t unique_id[128], int rank, int world) {
+std::unique_ptr<Exchange> make_rccl_exchange(const uint8_t unique_id[128], int rank, int world, double timeout_ms) {
   std::unique_ptr<RcclExchange> ex(new RcclExchange());
-  ncclUniqueId id;
-  std::memcpy(&id, unique_id, 128);
-  ZK_NCCL(ncclCommInitRank(&ex->comm, world, id, rank));
   ex->rank = rank;
   ex->world = world;
+  ex->timeout_ms = timeout_ms;
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id, 128);
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  const ncclResult_t r = ncclCommInitRankConfig(&ex->comm, world, id, rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    if (ex->comm) (void)ncclCommAbort(ex->comm);
+    ex->comm = nullptr;
+    throw Error(ZK_ERR_RCCL, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+  }
+  try {
+    nccl_wait(ex->comm, timeout_ms, "ncclCommInitRankConfig");
+  } catch (...) {
+    ex->abort();   // a half-made communicator: abort is local, destroy would wait for the peers
+    throw;
+  }
   return ex;
 }
 

@@ -36,6 +36,15 @@ struct Exchange {
   virtual void all_to_all(const void* send, void* recv, size_t chunk_bytes, hipStream_t st) = 0;
   // max over ranks of a host status code (synchronous)
   virtual int agree_max(int status, hipStream_t st) = 0;
+  // max over ranks of two host values at once (RCCL: one all-reduce of 2)
+  virtual void agree_max2(int32_t v[2], hipStream_t st) {
+    v[0] = agree_max(v[0], st);
+    v[1] = agree_max(v[1], st);
+  }
+  // max over ranks of the device word *d_val, enqueued on st without a host
+  // round trip; false when the transport cannot (the caller then agrees the
+  // value with agree_max once st is done)
+  virtual bool agree_max_dev(uint32_t* d_val, hipStream_t st) { (void)d_val; (void)st; return false; }
   // make the peers' pending collectives with this rank fail instead of
   // waiting forever (RCCL: ncclCommAbort; host: the caller's abort callback)
   virtual void abort() = 0;
@@ -78,8 +87,11 @@ void dist_quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, Exchan
 // a rank leaving its peers inside a collective).
 void dq_prepare(zk_ctx* ctx, const zk_pk_dev* pk, int world, DistQ& q, hipStream_t st);
 
-// RCCL communicator wrapper (ncclAllToAll, bytes as ncclUint8).
-std::unique_ptr<Exchange> make_rccl_exchange(const uint8_t unique_id[128], int rank, int world);
+// RCCL communicator wrapper (ncclAllToAll, bytes as ncclUint8).  The
+// communicator is non-blocking: its creation and every call on it are polled
+// with the watchdog, so a peer that never joins (or a transport that stalls)
+// ends in ZK_ERR_RCCL after timeout_ms instead of a hang.
+std::unique_ptr<Exchange> make_rccl_exchange(const uint8_t unique_id[128], int rank, int world, double timeout_ms);
 void rccl_unique_id(uint8_t out[128]);
 // Wait for stream st, polling: throws ZK_ERR_RCCL once ex's watchdog fires.
 void sync_watchdog(hipStream_t st, Exchange& ex);

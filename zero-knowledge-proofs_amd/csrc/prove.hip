@@ -527,9 +527,14 @@ static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipS
 // (three all-to-alls per proof).
 // zk_ctx_set_option(ZK_OPT_DIST_QUOTIENT, 0) turns it off: every rank then
 // computes the whole quotient (bench.py's replicated-quotient comparison).
-static bool uses_dist_quotient(const zk_ctx* ctx, const zk_pk_dev* pk) {
-  return ctx->dist_quotient != 0 && pk->nshards > 1 && ctx->exch && ctx->exch->world == (int)pk->nshards &&
+// exchange_matches: such an exchange is attached, whatever the option -- the
+// ranks then agree on the mode before every proof (prove_partial_common).
+static bool exchange_matches(const zk_ctx* ctx, const zk_pk_dev* pk) {
+  return pk->nshards > 1 && ctx->exch && ctx->exch->world == (int)pk->nshards &&
          ctx->exch->rank == (int)pk->shard && dist_quotient_ok(pk->n, (int)pk->nshards);
+}
+static bool uses_dist_quotient(const zk_ctx* ctx, const zk_pk_dev* pk) {
+  return ctx->dist_quotient != 0 && exchange_matches(ctx, pk);
 }
 
 // The G1 MSMs run as two batches (msm_launch_batch: one sort, accumulate,
@@ -758,6 +763,12 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   // finished its all-to-alls inside run_quotient, and only local GPU work
   // (RCCL: the enqueued collectives) is left
   const auto t_quot = clk::now();
+  // A distributed proof's witness checks are spread over the ranks (each
+  // checks its slice and its quotient rows): every rank takes the max of the
+  // flag words, so all return the status combine() would give -- flags are
+  // ORs of 8 (z_i >= r), 4 / 3 (InvalidWitness) and 2 (division), and the
+  // max keeps that precedence.  RCCL: on the stream, no host round trip.
+  const bool flags_agreed = dist && ctx->exch->agree_max_dev(ctx->flags.as<uint32_t>(), st);
   ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
   {
     const int h_slot[1] = {MSM_H};
@@ -820,7 +831,8 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   // host wall time of the whole call up to here, against prove_gpu_span
   ctx->prof.add_host("host_prove_total", ms_since(t_start));
   ctx->prof.collect();
-  const uint32_t flags = h_given ? given_flags : *ctx->flags_host.as<uint32_t>();
+  uint32_t flags = h_given ? given_flags : *ctx->flags_host.as<uint32_t>();
+  if (dist && !flags_agreed) flags = (uint32_t)ctx->exch->agree_max((int)flags, st);
   p.status = ZK_OK;
   if (flags & 8u) p.status = ZK_ERR_ARG;
   else if (flags & 5u) p.status = ZK_ERR_INVALID_WITNESS;
@@ -883,9 +895,10 @@ static int prove_partial_common(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_
   int local = ZK_OK;
   if (bad_slice || !fr_canonical(*r) || !fr_canonical(*s)) local = ZK_ERR_ARG;
   else if (num_public >= zlen || zlen != pk->V) local = ZK_ERR_INVALID_WITNESS;
+  const bool attached = exchange_matches(ctx, pk);
   const bool dist = uses_dist_quotient(ctx, pk);
-  if (dist && ctx->exch->broken) {
-    ctx->err = "the exchange was aborted by an earlier failed proof; attach a new one";
+  if (attached && ctx->exch->broken) {
+    ctx->err = "the exchange was aborted by an earlier failed proof; attach a new one (or detach it)";
     return ZK_ERR_RCCL;
   }
   hipStream_t st = ctx->stream;
@@ -901,7 +914,7 @@ static int prove_partial_common(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_
     }
     d_z = ctx->z_canon.p;
   };
-  if (!dist) {
+  if (!attached) {
     if (local == ZK_OK) {
       upload();
       p = prove_partial(ctx, pk, reinterpret_cast<const uint64_t*>(d_z), r, s, nullptr, 0, ranges);
@@ -911,14 +924,17 @@ static int prove_partial_common(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_
     std::memcpy(out->bytes, &p, sizeof p);
     return p.status;
   }
-  // Distributed quotient.  Every allocation it needs is made first, then
-  // the ranks agree on the host-side checks before the first all-to-all (a
-  // rank that bailed out alone would leave its peers blocked in the
-  // collective).  A failure after the agreement -- a transport error, a
-  // device error, a peer that stopped answering -- aborts the exchange, so
-  // the peers' pending transfers fail too, and marks it dead.
+  // An exchange of the key's shape is attached.  Every allocation a
+  // distributed quotient needs is made first, then the ranks agree on the
+  // host-side checks and on the quotient mode before the first all-to-all (a
+  // rank that bailed out alone, or one set to ZK_OPT_DIST_QUOTIENT 0 while
+  // its peers are not, would leave them blocked in the collective): one
+  // all-reduce of {any rank distributed, 2 status + any rank replicated}.
+  // A failure after the agreement -- a transport error, a device error, a
+  // peer that stopped answering -- aborts the exchange, so the peers'
+  // pending transfers fail too, and marks it dead.
   try {
-    if (local == ZK_OK) {
+    if (local == ZK_OK && dist) {
       try {
         dq_prepare(ctx, pk, (int)pk->nshards, ctx->dq, st);
         ctx->tmp_scal.ensure(sizeof(uint64_t) * (pk->n / pk->nshards));
@@ -928,8 +944,13 @@ static int prove_partial_common(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_
         ctx->err = e.what();
       }
     }
-    const int agreed = ctx->exch->agree_max(local, st);
-    if (local == ZK_OK) local = agreed;
+    int32_t v[2] = {dist ? 1 : 0, local * 2 + (dist ? 0 : 1)};
+    ctx->exch->agree_max2(v, st);
+    if (local == ZK_OK) local = v[1] >> 1;
+    if (local == ZK_OK && v[0] == 1 && (v[1] & 1)) {
+      local = ZK_ERR_ARG;
+      ctx->err = "ranks disagree on ZK_OPT_DIST_QUOTIENT: set it identically on every rank";
+    }
     if (local != ZK_OK) {
       p.status = local;
     } else {

@@ -638,15 +638,17 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_quant(MsmPlan p, con
 // 4..32 keep each lane's quad position) combines a wave, then a log2(RW)-step
 // tree over LDS combines the waves (wave w + 2^k hands its total to wave w
 // in step k).  One xyzz_add_quad call site.  The quantities (tens of sums)
-// always run on quads, G1 on ZK_QUANT_WAVES_G1 waves per sum (8: two waves
-// per SIMD at 189 VGPRs), G2 on ZK_RED_QWAVES (its 456 VGPRs allow one); the
+// always run on quads, G1 on ZK_QUANT_WAVES_G1 waves per sum (4: one wave per
+// SIMD, 2 terms per quad before the butterfly; round 5: prove 9.173 vs 9.252
+// ms with 8, median of 4 alternating processes, profiles/r05_ab_quant_waves.txt),
+// G2 on ZK_RED_QWAVES (its 456 VGPRs allow one); the
 // G1 row/column sums when there are few of them (ROWCOL_QUAD_MAX), on
 // ZK_RED_QWAVES waves.
 #ifndef ZK_RED_QWAVES
 #define ZK_RED_QWAVES 4
 #endif
 #ifndef ZK_QUANT_WAVES_G1
-#define ZK_QUANT_WAVES_G1 8
+#define ZK_QUANT_WAVES_G1 4
 #endif
 
 constexpr int ilog2_c(int x) { return x <= 1 ? 0 : 1 + ilog2_c(x / 2); }
@@ -982,6 +984,7 @@ static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hip
   if (pf) pf->end(st, ph);
   // The number of non-zero digits M' <= M is known on device only: the T
   // accumulate threads split it evenly there (chunk_len), no host sync.
+  if (w.wait_accum) ZK_HIP(hipStreamWaitEvent(st, w.wait_accum, 0));
   if (M) {
     ph = pf ? pf->begin(st, (w.tag + (g2 ? "msm_accum_g2" : "msm_accum_g1")).c_str(), n) : -1;
     if constexpr (g2)

@@ -984,7 +984,6 @@ static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hip
   if (pf) pf->end(st, ph);
   // The number of non-zero digits M' <= M is known on device only: the T
   // accumulate threads split it evenly there (chunk_len), no host sync.
-  if (w.wait_accum) ZK_HIP(hipStreamWaitEvent(st, w.wait_accum, 0));
   if (M) {
     ph = pf ? pf->begin(st, (w.tag + (g2 ? "msm_accum_g2" : "msm_accum_g1")).c_str(), n) : -1;
     if constexpr (g2)

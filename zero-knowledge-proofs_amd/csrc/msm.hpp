@@ -104,7 +104,6 @@ struct MsmWork {
   PinnedBuf host_res;
   MsmPlan plan{};
   Prof* prof = nullptr;  // optional live kernel timing
-  hipEvent_t wait_accum = nullptr;   // optional: the accumulate waits for this event (sort runs ahead)
   std::string tag;      // phase-name prefix (per-MSM profiling)
 };
 

@@ -542,9 +542,6 @@ static bool uses_dist_quotient(const zk_ctx* ctx, const zk_pk_dev* pk) {
 // tree depth per batch): A, B1 and IC need only z and start with the
 // witness; H follows the quotient.
 static const int G1_ABI[3] = {MSM_A, MSM_B1, MSM_IC};
-#ifndef ZK_ABI_AFTER_QUOT
-#define ZK_ABI_AFTER_QUOT 0
-#endif
 
 // h_given (virtual-rank tests): this shard's lo64(H_(shard + nshards d)) is
 // already on the device, with the witness-check flags of all ranks.
@@ -733,7 +730,6 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   // streams wait for it, so its all-to-alls find free CUs on every rank.
   // (Split uploads are single-GPU only: the quotient needs all of z.)
   const bool xfirst = dist && ctx->exchange_first == 1 && !serial && !split;
-  bool quot_done = false;
   if (xfirst) {
     run_quotient();
     ZK_HIP(hipEventRecord(ctx->ev_quot, st));
@@ -759,32 +755,10 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       ZK_HIP(hipStreamWaitEvent(s_abi, ctx->ev_scal, 0));
     }
     launch_part(1, s_g2, s_abi);
-  } else if (ZK_ABI_AFTER_QUOT && !dist && !serial && !h_given) {
-    // A/B: G2 first, then the quotient, then the A+B1+IC keys and sort, whose
-    // accumulate waits for the quotient (so the last quotient NTT is not
-    // starved by that full-occupancy round and H follows it at once)
-    if (!serial) ZK_HIP(hipStreamWaitEvent(s_g2, ctx->ev_scal, 0));
-    {
-      Range range("msm_g2");
-      MsmWork& w = ctx->msm[MSM_B2];
-      w.tag = "";
-      prep_scalars(MSM_B2, s_g2);
-      msm_launch_shared<G2>(w, pk->bases[MSM_B2].as<G2A>(), ctx->scal[MSM_B2].as<uint64_t>(), 1,
-                            pk->count[MSM_B2] + pk->extras[MSM_B2], 64, pk->win_c, s_g2, pk->stride[MSM_B2]);
-      msm_download<G2>(w, s_g2);
-      ZK_HIP(hipEventRecord(ctx->ev_done[MSM_B2], s_g2));
-    }
-    run_quotient();
-    ZK_HIP(hipEventRecord(ctx->ev_quot, st));
-    ZK_HIP(hipStreamWaitEvent(s_abi, ctx->ev_scal, 0));
-    ctx->msm[MSM_A].wait_accum = ctx->ev_quot;
-    launch_batch(G1_ABI, 3, "ABI/", s_abi);
-    ctx->msm[MSM_A].wait_accum = nullptr;
-    quot_done = true;
   } else {
     launch_msms();
   }
-  if (!xfirst && !quot_done) run_quotient();
+  if (!xfirst) run_quotient();
   // the exchange watchdog below counts from here: a host-staged exchange has
   // finished its all-to-alls inside run_quotient, and only local GPU work
   // (RCCL: the enqueued collectives) is left

@@ -54,7 +54,8 @@ zk_ctx* zk_ctx_create(int device) {
     ZK_HIP(hipSetDevice(device));
     std::unique_ptr<zk_ctx> c(new zk_ctx());
     c->device = device;
-    for (int i = 0; i < NUM_MSM; i++) c->msm[i].prof = c->msm2[i].prof = &c->prof;
+    for (int i = 0; i < NUM_MSM; i++) c->msm[i].prof = &c->prof;
+    for (int k = 0; k < HOST_PARTS - 1; k++) c->part_g2[k].prof = c->part_abi[k].prof = &c->prof;
     int lo_prio = 0, hi_prio = 0;
     ZK_HIP(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
     ZK_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio));   // quotient + H

@@ -14,6 +14,13 @@ namespace zk {
 
 constexpr int NUM_MSM = 5;  // pi_A (G1), pi_B (G2), B1 (G1), IC (G1), H (G1)
 constexpr int NUM_SIDE = 3; // side streams (+ main = 4 = GPU_MAX_HW_QUEUES)
+// Parts of a host witness upload (zk_groth16_prove): part k's MSMs run while
+// part k+1 is still crossing PCIe (pk_part_cuts).
+#ifndef ZK_HOST_PARTS
+#define ZK_HOST_PARTS 2
+#endif
+constexpr int HOST_PARTS = ZK_HOST_PARTS;
+static_assert(HOST_PARTS >= 2 && HOST_PARTS <= 6, "host witness parts");
 enum MsmSlot { MSM_A = 0, MSM_B2 = 1, MSM_B1 = 2, MSM_IC = 3, MSM_H = 4 };
 
 // Device copy of the constraint matrices (the QAP in sparse form).
@@ -34,7 +41,11 @@ struct zk_ctx {
   hipEvent_t ev_done[zk::NUM_MSM] = {};         // per-MSM completion (results downloaded)
   std::string err;
   zk::MsmWork msm[zk::NUM_MSM];
-  zk::MsmWork msm2[zk::NUM_MSM];                // first parts of MSMs split over a host witness upload
+  // the G2 and A+B1+IC MSMs' workspaces for every part of a host witness
+  // upload but the last (which uses msm[]): buckets, keys and sort scratch
+  // of each part stay allocated, ~60 MB per part at 2^20 constraints (c = 16)
+  // and ~2 GB at 2^24 (c = 22: 2^21 buckets per MSM)
+  zk::MsmWork part_g2[zk::HOST_PARTS - 1], part_abi[zk::HOST_PARTS - 1];
   std::map<uint32_t, std::unique_ptr<zk::NttDomain>> domains;
   // prove scratch
   zk::DevBuf z_canon, qabc, flags;   // qabc: the quotient's A, B, C vectors back to back (3n)
@@ -78,12 +89,12 @@ struct zk_pk_dev {
   // [lo, hi) pairs: the z entries this shard reads with a distributed
   // quotient (zk_groth16_witness_ranges); without one it reads all of z
   std::vector<uint64_t> wr_dist;
-  // Host-witness prove (zk_groth16_prove): z crosses PCIe in two parts,
-  // variables [0, vh) then [vh, V); cut[slot] = compacted bases whose
-  // variable is < vh, so the first part's MSMs start while the second part
-  // is still in flight (pk_part_cuts).
-  uint64_t vh = 0;
-  uint32_t cut[zk::NUM_MSM] = {};
+  // Host-witness prove (zk_groth16_prove): z crosses PCIe in HOST_PARTS
+  // parts, variables [vcut[k], vcut[k+1]); pcut[k][slot] = compacted bases
+  // whose variable is < vcut[k], so part k's MSMs run while part k+1 is still
+  // in flight (pk_part_cuts).
+  uint64_t vcut[zk::HOST_PARTS + 1] = {};
+  uint32_t pcut[zk::HOST_PARTS + 1][zk::NUM_MSM] = {};
 };
 
 namespace zk {
@@ -94,7 +105,7 @@ void pk_precompute_windows(zk_ctx* ctx, zk_pk_dev& pk);
 // flags |= 8 when some of the n canonical Fr at d_z is >= r
 bool fr_canonical(const zk_fr& a);
 void check_canonical(const void* d_z, uint64_t n, uint32_t* d_flags, hipStream_t st);
-// vh and cut[] of a finished key (device binary search over its idx vectors)
+// vcut and pcut of a finished key (device binary search over its idx vectors)
 void pk_part_cuts(zk_pk_dev& pk, hipStream_t st);
 // the witness ranges of a finished key (its idx vectors and shard) from the
 // host constraint matrices: fills pk.wr_dist

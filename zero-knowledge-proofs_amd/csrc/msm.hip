@@ -791,9 +791,11 @@ __global__ void __launch_bounds__(128) k_msm_fixup_pair(const uint32_t* __restri
 // part's bucket + the earlier part's, each only where its part had entries,
 // written for EVERY bucket (infinity where both are empty), so the reduction
 // reads them all (MsmPlan::all_valid).
+// prev_all: the earlier part's every bucket holds a value (it combined
+// with a part before it).
 template <class C>
 __global__ void __launch_bounds__(128) k_msm_combine(const uint32_t* __restrict__ off,
-                                                     const uint32_t* __restrict__ off_prev, uint32_t G,
+                                                     const uint32_t* __restrict__ off_prev, bool prev_all, uint32_t G,
                                                      typename C::X* __restrict__ buckets,
                                                      const typename C::X* __restrict__ prev) {
   using X = typename C::X;
@@ -802,19 +804,20 @@ __global__ void __launch_bounds__(128) k_msm_combine(const uint32_t* __restrict_
   X a, b;
   if (off[g + 1] != off[g]) a = ld_vec(&buckets[g]);
   else xyzz_set_inf(a);
-  if (off_prev[g + 1] != off_prev[g]) b = ld_vec(&prev[g]);
+  if (prev_all || off_prev[g + 1] != off_prev[g]) b = ld_vec(&prev[g]);
   else xyzz_set_inf(b);
   st_vec(&buckets[g], tail_add(a, b));
 }
 __global__ void __launch_bounds__(128) k_msm_combine_pair(const uint32_t* __restrict__ off,
-                                                          const uint32_t* __restrict__ off_prev, uint32_t G,
-                                                          G2X* __restrict__ buckets, const G2X* __restrict__ prev) {
+                                                          const uint32_t* __restrict__ off_prev, bool prev_all,
+                                                          uint32_t G, G2X* __restrict__ buckets,
+                                                          const G2X* __restrict__ prev) {
   const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
   if (g >= G) return;   // pair-uniform
   XYZZ<Fq2h> a, b;
   if (off[g + 1] != off[g]) a = ld_pair(&buckets[g]);
   else xyzz_set_inf(a);
-  if (off_prev[g + 1] != off_prev[g]) b = ld_pair(&prev[g]);
+  if (prev_all || off_prev[g + 1] != off_prev[g]) b = ld_pair(&prev[g]);
   else xyzz_set_inf(b);
   st_pair(&buckets[g], tail_add(a, b));
 }
@@ -1041,20 +1044,21 @@ static void msm_back_impl(MsmWork& w, hipStream_t st, int mode, const MsmWork* p
     }
   }
   p.all_valid = 0;
-  if (mode == MSM_BACK_COMBINE) {
+  if (mode == MSM_BACK_COMBINE || mode == MSM_BACK_ACCUM) {
     if (!prev || prev->plan.G != p.G || prev->plan.nseg != p.nseg) throw Error(ZK_ERR_ARG, "msm: combine plans differ");
+    const bool prev_all = prev->plan.all_valid != 0;
     if constexpr (g2)
       k_msm_combine_pair<<<ceil_div(2 * (size_t)p.G, 128), 128, 0, st>>>(
-          w.off.as<uint32_t>(), prev->off.as<uint32_t>(), p.G, reinterpret_cast<G2X*>(w.buckets.p),
+          w.off.as<uint32_t>(), prev->off.as<uint32_t>(), prev_all, p.G, reinterpret_cast<G2X*>(w.buckets.p),
           reinterpret_cast<const G2X*>(prev->buckets.p));
     else
-      k_msm_combine<C><<<ceil_div(p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), prev->off.as<uint32_t>(), p.G,
-                                                            w.buckets.as<X>(), prev->buckets.as<X>());
+      k_msm_combine<C><<<ceil_div(p.G, 128), 128, 0, st>>>(w.off.as<uint32_t>(), prev->off.as<uint32_t>(), prev_all,
+                                                            p.G, w.buckets.as<X>(), prev->buckets.as<X>());
     ZK_LAUNCH_CHECK();
     p.all_valid = 1;
   }
   if (pf) pf->end(st, ph);
-  if (mode == MSM_BACK_FIXUP) return;
+  if (mode == MSM_BACK_FIXUP || mode == MSM_BACK_ACCUM) return;
   ph = pf ? pf->begin(st, (w.tag + "msm_bucket_sum").c_str(), p.G) : -1;   // row/col sums + quantities
   constexpr int RW = ZK_RED_QWAVES;
   if constexpr (g2)

@@ -126,11 +126,12 @@ void msm_launch_batch(MsmWork& w, const MsmSeg* segs, int nseg, int bits, int c,
 // The same in two halves, for an MSM whose points arrive in parts: the
 // front (keys, sort, accumulate) and the back (bucket fixup / merge, then
 // the bucket reduction).  back modes: MSM_BACK_FULL (msm_launch_batch),
-// MSM_BACK_FIXUP (complete the buckets only: the first part of a split MSM)
-// and MSM_BACK_COMBINE (complete the buckets, add the completed buckets of
-// `prev` -- an earlier part over the same plan, already past its FIXUP back
-// on this stream or one it waited for -- then reduce: the sum of both parts).
-enum { MSM_BACK_FULL = 0, MSM_BACK_FIXUP = 1, MSM_BACK_COMBINE = 2 };
+// MSM_BACK_FIXUP (complete the buckets only: the first part of a split MSM),
+// MSM_BACK_ACCUM (complete the buckets and add the completed buckets of
+// `prev` -- an earlier part over the same plan, already past its own back on
+// this stream -- into every bucket: a middle part) and MSM_BACK_COMBINE (the
+// same, then reduce: the last part, the sum of all parts).
+enum { MSM_BACK_FULL = 0, MSM_BACK_FIXUP = 1, MSM_BACK_COMBINE = 2, MSM_BACK_ACCUM = 3 };
 template <class C>
 void msm_batch_front(MsmWork& w, const MsmSeg* segs, int nseg, int bits, int c, hipStream_t st);
 template <class C>

@@ -314,27 +314,44 @@ __global__ void k_lower_bound(const uint32_t* __restrict__ idx, uint32_t count, 
   *out = lo;
 }
 
-// The first part of a host witness is 1/ZK_HOST_SPLIT_DIV of it: its MSM
-// share then starts after a third of the copy and still outlasts the rest
-// of it.  Host-witness minus device-witness prove at 2^20 (medians of 3,
-// tools/pcie_ab.py, profiles/r04_ab_host_split.txt): 1/2 +1.33 ms, 1/3
-// +0.84, 1/4 +0.86, 1/6 +1.29; one whole copy before the prove was +2.5.
-// (ZK_HOST_SPLIT_DIV: A/B builds only, tools/build_variant.sh.)
-#ifndef ZK_HOST_SPLIT_DIV
-#define ZK_HOST_SPLIT_DIV 3
+// The parts of a host witness grow geometrically, ZK_HOST_PART_RATIO times
+// each (2 parts, ratio 2: the first third, then the rest): the MSM work of
+// the parts already on the device outlasts the copy of the next one.  Every
+// part costs its own sort, bucket fixup and combine on the G2 and A+B1+IC
+// streams, so more, smaller parts lose what the smaller exposed first copy
+// saves.  Host-witness minus device-witness prove at 2^20 (tools/pcie_ab.py,
+// medians of 4 alternating processes, profiles/r05_ab_host_parts.txt): 2
+// parts +0.864 ms, 3 parts (ratio 3) +1.042, 4 parts (ratio 2.5) +1.231;
+// round 4 with 2 parts, first part 1/2 +1.33, 1/3 +0.84, 1/4 +0.86, 1/6 +1.29
+// (profiles/r04_ab_host_split.txt).  (ZK_HOST_PARTS / ZK_HOST_PART_RATIO:
+// A/B builds only.)
+#ifndef ZK_HOST_PART_RATIO
+#define ZK_HOST_PART_RATIO 2
 #endif
 void pk_part_cuts(zk_pk_dev& pk, hipStream_t st) {
-  pk.vh = pk.V / ZK_HOST_SPLIT_DIV;
+  double w = 1, tot = 0;
+  double f[HOST_PARTS];
+  for (int k = 0; k < HOST_PARTS; k++, w *= ZK_HOST_PART_RATIO) tot += (f[k] = w);
+  double acc = 0;
+  pk.vcut[0] = 0;
+  for (int k = 1; k < HOST_PARTS; k++) {
+    acc += f[k - 1] / tot;
+    pk.vcut[k] = std::max<uint64_t>(pk.vcut[k - 1], (uint64_t)(acc * (double)pk.V));
+  }
+  pk.vcut[HOST_PARTS] = pk.V;
   DevBuf d;
-  d.ensure(sizeof(uint32_t) * NUM_MSM);
-  ZK_HIP(hipMemsetAsync(d.p, 0, sizeof(uint32_t) * NUM_MSM, st));
-  for (int slot : {MSM_A, MSM_B2, MSM_B1, MSM_IC})
-    if (pk.count[slot]) {
-      k_lower_bound<<<1, 1, 0, st>>>(pk.idx[slot].as<uint32_t>(), pk.count[slot], pk.vh, d.as<uint32_t>() + slot);
-      ZK_LAUNCH_CHECK();
-    }
-  ZK_HIP(hipMemcpyAsync(pk.cut, d.p, sizeof(uint32_t) * NUM_MSM, hipMemcpyDeviceToHost, st));
+  d.ensure(sizeof(uint32_t) * NUM_MSM * (HOST_PARTS + 1));
+  ZK_HIP(hipMemsetAsync(d.p, 0, sizeof(uint32_t) * NUM_MSM * (HOST_PARTS + 1), st));
+  for (int k = 1; k < HOST_PARTS; k++)
+    for (int slot : {MSM_A, MSM_B2, MSM_B1, MSM_IC})
+      if (pk.count[slot]) {
+        k_lower_bound<<<1, 1, 0, st>>>(pk.idx[slot].as<uint32_t>(), pk.count[slot], pk.vcut[k],
+                                       d.as<uint32_t>() + k * NUM_MSM + slot);
+        ZK_LAUNCH_CHECK();
+      }
+  ZK_HIP(hipMemcpyAsync(pk.pcut, d.p, sizeof(uint32_t) * NUM_MSM * (HOST_PARTS + 1), hipMemcpyDeviceToHost, st));
   ZK_HIP(hipStreamSynchronize(st));
+  for (int slot = 0; slot < NUM_MSM; slot++) pk.pcut[HOST_PARTS][slot] = pk.count[slot];
 }
 
 std::vector<uint8_t> var_owner(const zk_r1cs_csr* q, uint64_t n, uint32_t N) {
@@ -552,11 +569,11 @@ static const int G1_ABI[3] = {MSM_A, MSM_B1, MSM_IC};
 // a field inversion (~40 us on one core) that would otherwise follow the
 // last MSM.
 // z_host (the drop-in host-witness prove): d_z is the ctx's device copy,
-// filled here in two parts -- variables [0, vh), then [vh, V) -- and the
-// G2 and A+B1+IC MSMs run split the same way: the first part's keys, sort
-// and accumulate start as soon as its half of z has landed, while the second
-// half is still crossing PCIe; the second part then adds the first part's
-// completed buckets (msm_batch_back COMBINE) and reduces once.
+// filled here in HOST_PARTS parts (pk_part_cuts) -- and the G2 and A+B1+IC
+// MSMs run split the same way: part k's keys, sort and accumulate start as
+// soon as its slice of z has landed, while the next slice is still crossing
+// PCIe; each later part adds the previous part's completed buckets
+// (msm_batch_back ACCUM / COMBINE) and the last one reduces once.
 static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, const zk_fr* r,
                              const zk_fr* s, const uint64_t* h_given = nullptr, uint32_t given_flags = 0,
                              const std::vector<uint64_t>* ranges = nullptr, zk_proof* early = nullptr,
@@ -572,10 +589,17 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   const int ph_span = ctx->prof.begin(st, "prove_gpu_span", pk->n);   // first kernel .. last MSM done
   ZK_HIP(hipMemsetAsync(ctx->flags.p, 0, 16, st));
   const bool split = z_host != nullptr;
-  const uint64_t vh = split ? pk->vh : 0;
-  if (split) {   // first part of z; every z_i < r, else ZK_ERR_ARG
-    if (vh) ZK_HIP(hipMemcpyAsync(const_cast<uint64_t*>(d_z), z_host, sizeof(zk_fr) * vh, hipMemcpyHostToDevice, st));
-    check_canonical(d_z, vh, ctx->flags.as<uint32_t>(), st);
+  // part k of a host witness: variables [vcut[k], vcut[k+1]) to the device,
+  // every z_i < r, else ZK_ERR_ARG (the host thread waits for a pageable copy)
+  auto upload_part = [&](int k) {
+    const uint64_t lo = pk->vcut[k], hi = pk->vcut[k + 1];
+    if (hi > lo)
+      ZK_HIP(hipMemcpyAsync(const_cast<uint64_t*>(d_z) + 4 * lo, z_host + lo, sizeof(zk_fr) * (hi - lo),
+                            hipMemcpyHostToDevice, st));
+    check_canonical(d_z + 4 * lo, hi - lo, ctx->flags.as<uint32_t>(), st);
+  };
+  if (split) {
+    upload_part(0);
   } else if (ranges) {   // every z_i < r, else ZK_ERR_ARG
     for (size_t k = 0; k + 1 < ranges->size(); k += 2)
       check_canonical(reinterpret_cast<const Fr*>(d_z) + (*ranges)[k], (*ranges)[k + 1] - (*ranges)[k],
@@ -645,36 +669,41 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
     sg.ioff = lo;
     return sg;
   };
-  // part 0: positions [0, cut); part 1: [cut, count + extras)
+  // part k: compacted positions [pcut[k], pcut[k+1]) of every slot, the
+  // extras with the last part.  Part 0 completes its buckets (FIXUP), every
+  // later part adds the previous part's (ACCUM), and the last one reduces
+  // (COMBINE).
   auto launch_part = [&](int part, hipStream_t gs2, hipStream_t gsa) {
+    const bool last = part == HOST_PARTS - 1;
+    const int mode = part == 0 ? MSM_BACK_FIXUP : last ? MSM_BACK_COMBINE : MSM_BACK_ACCUM;
     {
-      Range range(part ? "msm_g2_part1" : "msm_g2_part0");
-      const uint32_t c = pk->cut[MSM_B2], tot = pk->count[MSM_B2] + pk->extras[MSM_B2];
-      MsmWork& w = part ? ctx->msm[MSM_B2] : ctx->msm2[MSM_B2];
-      w.tag = serial ? (part ? "B2/" : "B2a/") : "";
-      prep_range(MSM_B2, part ? c : 0, part ? pk->count[MSM_B2] : c, part == 1, gs2);
-      const MsmSeg sg = seg_range(MSM_B2, part ? c : 0, part ? tot : c);
+      Range range("msm_g2_part");
+      const uint32_t lo = pk->pcut[part][MSM_B2], hi = pk->pcut[part + 1][MSM_B2];
+      MsmWork& w = last ? ctx->msm[MSM_B2] : ctx->part_g2[part];
+      w.tag = serial ? (last ? "B2/" : "B2p/") : "";
+      prep_range(MSM_B2, lo, hi, last, gs2);
+      const MsmSeg sg = seg_range(MSM_B2, lo, last ? hi + pk->extras[MSM_B2] : hi);
       msm_batch_front<G2>(w, &sg, 1, 64, pk->win_c, gs2);
-      msm_batch_back<G2>(w, gs2, part ? MSM_BACK_COMBINE : MSM_BACK_FIXUP, part ? &ctx->msm2[MSM_B2] : nullptr);
-      if (part) {
+      msm_batch_back<G2>(w, gs2, mode, part ? &ctx->part_g2[part - 1] : nullptr);
+      if (last) {
         msm_download<G2>(w, gs2);
         ZK_HIP(hipEventRecord(ctx->ev_done[MSM_B2], gs2));
       }
     }
     {
-      Range range(part ? "msm_g1_a_b1_ic_part1" : "msm_g1_a_b1_ic_part0");
+      Range range("msm_g1_a_b1_ic_part");
       MsmSeg segs[3];
       for (int i = 0; i < 3; i++) {
         const int sl = G1_ABI[i];
-        const uint32_t c = pk->cut[sl], tot = pk->count[sl] + pk->extras[sl];
-        prep_range(sl, part ? c : 0, part ? pk->count[sl] : c, part == 1, gsa);
-        segs[i] = seg_range(sl, part ? c : 0, part ? tot : c);
+        const uint32_t lo = pk->pcut[part][sl], hi = pk->pcut[part + 1][sl];
+        prep_range(sl, lo, hi, last, gsa);
+        segs[i] = seg_range(sl, lo, last ? hi + pk->extras[sl] : hi);
       }
-      MsmWork& w = part ? ctx->msm[MSM_A] : ctx->msm2[MSM_A];
-      w.tag = serial ? (part ? "ABI/" : "ABIa/") : "";
+      MsmWork& w = last ? ctx->msm[MSM_A] : ctx->part_abi[part];
+      w.tag = serial ? (last ? "ABI/" : "ABIp/") : "";
       msm_batch_front<G1>(w, segs, 3, 64, pk->win_c, gsa);
-      msm_batch_back<G1>(w, gsa, part ? MSM_BACK_COMBINE : MSM_BACK_FIXUP, part ? &ctx->msm2[MSM_A] : nullptr);
-      if (part) {
+      msm_batch_back<G1>(w, gsa, mode, part ? &ctx->part_abi[part - 1] : nullptr);
+      if (last) {
         msm_download<G1>(w, gsa);
         ZK_HIP(hipEventRecord(ctx->ev_done[MSM_A], gsa));
       }
@@ -737,24 +766,19 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
     ZK_HIP(hipStreamWaitEvent(s_abi, ctx->ev_quot, 0));
   }
   if (split) {
-    if (!serial) {
-      ZK_HIP(hipStreamWaitEvent(s_g2, ctx->ev_scal, 0));
-      ZK_HIP(hipStreamWaitEvent(s_abi, ctx->ev_scal, 0));
+    // part k's MSMs, then part k+1 of z (the host thread waits for the
+    // pageable copy while the GPU runs the parts already there)
+    for (int k = 0; k < HOST_PARTS; k++) {
+      if (k) {
+        upload_part(k);
+        ZK_HIP(hipEventRecord(ctx->ev_scal, st));
+      }
+      if (!serial) {
+        ZK_HIP(hipStreamWaitEvent(s_g2, ctx->ev_scal, 0));
+        ZK_HIP(hipStreamWaitEvent(s_abi, ctx->ev_scal, 0));
+      }
+      launch_part(k, s_g2, s_abi);
     }
-    launch_part(0, s_g2, s_abi);
-    // second part of z (the host thread waits for the pageable copy while
-    // the GPU runs the first part's MSMs), then its MSMs
-    const uint64_t V = pk->V;
-    if (V > vh)
-      ZK_HIP(hipMemcpyAsync(const_cast<uint64_t*>(d_z) + 4 * vh, z_host + vh, sizeof(zk_fr) * (V - vh),
-                            hipMemcpyHostToDevice, st));
-    check_canonical(d_z + 4 * vh, V - vh, ctx->flags.as<uint32_t>(), st);
-    ZK_HIP(hipEventRecord(ctx->ev_scal, st));
-    if (!serial) {
-      ZK_HIP(hipStreamWaitEvent(s_g2, ctx->ev_scal, 0));
-      ZK_HIP(hipStreamWaitEvent(s_abi, ctx->ev_scal, 0));
-    }
-    launch_part(1, s_g2, s_abi);
   } else {
     launch_msms();
   }

@@ -61,8 +61,13 @@ zk_ctx* zk_ctx_create(int device) {
     ZK_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio));   // quotient + H
     // side[0]: G2 MSM (high), side[1..]: the G1 batches (low); other
     // priority assignments measured within noise
+    // (ZK_SIDE_PRIO_MASK: A/B builds, bit i = side[i] at high priority)
+#ifndef ZK_SIDE_PRIO_MASK
+#define ZK_SIDE_PRIO_MASK 1
+#endif
     for (int i = 0; i < NUM_SIDE; i++)
-      ZK_HIP(hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking, i == 0 ? hi_prio : lo_prio));
+      ZK_HIP(hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking,
+                                         (ZK_SIDE_PRIO_MASK >> i) & 1 ? hi_prio : lo_prio));
     ZK_HIP(hipEventCreateWithFlags(&c->ev_scal, hipEventDisableTiming));
     ZK_HIP(hipEventCreateWithFlags(&c->ev_quot, hipEventDisableTiming));
     for (auto& e : c->ev_done) ZK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));

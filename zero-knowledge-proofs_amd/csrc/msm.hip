@@ -943,7 +943,7 @@ static void msm_split_sums(MsmPlan& p, uint32_t target, uint32_t lanes) {
 // Lane-quad fixup for plans with >= 2 chunks per bucket (ZK_FIXUP_QUAD=0:
 // A/B build without it)
 #ifndef ZK_FIXUP_QUAD
-#define ZK_FIXUP_QUAD 1
+#define ZK_FIXUP_QUAD 0
 #endif
 
 // Buckets spread over at most this many accumulate chunks are summed by the

@@ -17,12 +17,20 @@ namespace zk {
 #ifndef ZK_SORT_MAX_BITS
 #define ZK_SORT_MAX_BITS 10
 #endif
+// Onesweep block shape (ZK_SORT_BLOCK threads x ZK_SORT_ITEMS items; A/B
+// builds only).
+#ifndef ZK_SORT_BLOCK
+#define ZK_SORT_BLOCK 1024
+#endif
+#ifndef ZK_SORT_ITEMS
+#define ZK_SORT_ITEMS 16
+#endif
 template <unsigned R>
-using OnesweepCfg =
-    rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                               rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>,
-                                                                   rocprim::kernel_config<1024, 16>, R,
-                                                                   rocprim::block_radix_rank_algorithm::match>>;
+using OnesweepCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<ZK_SORT_BLOCK, ZK_SORT_ITEMS>,
+                                        rocprim::kernel_config<ZK_SORT_BLOCK, ZK_SORT_ITEMS>, R,
+                                        rocprim::block_radix_rank_algorithm::match>>;
 
 template <unsigned R>
 static hipError_t sort_r(void* tmp, size_t& tmp_bytes, const uint32_t* ki, uint32_t* ko, const uint32_t* vi,

@@ -467,34 +467,6 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
   st_vec(&buckets[g], acc);
 }
 
-// The same over lane quads (xyzz_add_quad: each add split over the quad's 4
-// lanes) for MSMs with many chunks per bucket -- few buckets, several pieces
-// each (the H MSM at 2^20: 65536 buckets over 196608 chunks, 3 serial adds
-// per bucket on a third of the chip), where a one-lane chain's latency sets
-// the launch's time.
-template <class C>
-__global__ void __launch_bounds__(128) k_msm_fixup_q(const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
-                                                     uint32_t fix_max, uint32_t* __restrict__ nbig,
-                                                     typename C::X* __restrict__ buckets,
-                                                     const typename C::X* __restrict__ partials) {
-  using X = typename C::X;
-  const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;
-  if (g >= G) return;   // quad-uniform from here on
-  const uint32_t K = chunk_len(off[G], T);
-  const uint32_t bs = off[g], be = off[g + 1];
-  if (be == bs) return;
-  const uint32_t t0 = bs / K, t1 = (be - 1) / K;
-  if (t0 == t1) return;
-  if (t1 - t0 + 1 > fix_max) {
-    if ((threadIdx.x & 3) == 0) atomicAdd(nbig, 1u);
-    return;
-  }
-  X acc = ld_vec(&partials[2 * (size_t)t0 + 1]);
-#pragma unroll 1
-  for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add_quad(acc, ld_vec(&partials[2 * (size_t)t]));
-  if ((threadIdx.x & 3) == 0) st_vec(&buckets[g], acc);
-}
-
 template <class X>
 __device__ __forceinline__ X shfl_xor_point(const X& v, int d) {
   constexpr int NW = sizeof(X) / 4;
@@ -940,12 +912,6 @@ static void msm_split_sums(MsmPlan& p, uint32_t target, uint32_t lanes) {
   }
 }
 
-// Lane-quad fixup for plans with >= 2 chunks per bucket (ZK_FIXUP_QUAD=0:
-// A/B build without it)
-#ifndef ZK_FIXUP_QUAD
-#define ZK_FIXUP_QUAD 0
-#endif
-
 // Buckets spread over at most this many accumulate chunks are summed by the
 // serial fixup; larger ones go through the log-depth merge.
 constexpr uint32_t MSM_FIX_MAX = 8;
@@ -1053,9 +1019,6 @@ static void msm_back_impl(MsmWork& w, hipStream_t st, int mode, const MsmWork* p
     k_msm_fixup_pair<<<ceil_div(2 * (size_t)p.G, 128), 128, 0, st>>>(
         w.off.as<uint32_t>(), p.G, p.T, p.fix_max, w.nbig.as<uint32_t>(), reinterpret_cast<G2X*>(w.buckets.p),
         reinterpret_cast<const G2X*>(w.partials.p));
-  else if (ZK_FIXUP_QUAD && (uint64_t)p.T >= 2ull * p.G)   // >= 3 pieces per bucket on average
-    k_msm_fixup_q<C><<<ceil_div(4 * (size_t)p.G, 128), 128, 0, st>>>(
-        w.off.as<uint32_t>(), p.G, p.T, p.fix_max, w.nbig.as<uint32_t>(), w.buckets.as<X>(), w.partials.as<X>());
   else
   {
     const bool by_boundary = p.G > p.T;

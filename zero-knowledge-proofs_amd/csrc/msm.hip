@@ -126,7 +126,6 @@ __device__ __forceinline__ uint32_t scal_window(const uint64_t (&s)[SW], int off
   return (uint32_t)(lo & ((1ull << width) - 1));
 }
 
-constexpr uint32_t MSM_DUMMY = 0x7fffffffu;   // entry that contributes nothing
 
 // Radix-sort path: one (bucket, entry) pair per (point, window), written
 // window-major (coalesced); a zero digit gets the key G, which sorts after
@@ -433,6 +432,26 @@ __device__ __forceinline__ bool big_bucket(const uint32_t* off, uint32_t b, uint
   return (off[b + 1] - 1) / K - off[b] / K + 1 > fix_max;
 }
 
+// Fixup deferral (ZK_FIXUP_DEFER, plans whose buckets mostly span two
+// chunks): the first pass does only the one-add buckets, so each of its
+// waves runs one add instead of its slowest lane's two or three (~4 % of the
+// buckets span three chunks, but nearly every wave holds one); the others
+// are listed (wave-aggregated atomic) for k_msm_fixup_rest.  Returns whether
+// the lane's bucket was deferred.
+#ifndef ZK_FIXUP_DEFER
+#define ZK_FIXUP_DEFER 0
+#endif
+ZK_DI bool fixup_defer(bool d, uint32_t g, uint32_t* __restrict__ defer, uint32_t* __restrict__ cnt) {
+  const uint64_t m = __ballot(d);
+  if (!m) return false;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  uint32_t base = 0;
+  if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+  base = __shfl(base, leader);
+  if (d) defer[base + __popcll(m & ((1ull << (threadIdx.x & 63)) - 1))] = g;
+  return d;
+}
+
 // One thread per bucket, or -- when there are more buckets than chunks
 // (by_boundary: the 2^19-bucket full-width MSM, where most buckets lie inside
 // one chunk and most per-bucket lanes would idle) one thread per chunk
@@ -441,7 +460,8 @@ __device__ __forceinline__ bool big_bucket(const uint32_t* off, uint32_t b, uint
 template <class C>
 __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ key, const uint32_t* __restrict__ off,
                                                    uint32_t G, uint32_t T, uint32_t fix_max, bool by_boundary,
-                                                   uint32_t* __restrict__ nbig, typename C::X* __restrict__ buckets,
+                                                   uint32_t* __restrict__ nbig, uint32_t* __restrict__ defer,
+                                                   typename C::X* __restrict__ buckets,
                                                    const typename C::X* __restrict__ partials) {
   using X = typename C::X;
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
@@ -462,9 +482,31 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
     atomicAdd(nbig, 1u);
     return;
   }
+  if (defer && fixup_defer(t1 - t0 >= 2, g, defer, nbig + 2)) return;
   X acc = ld_vec(&partials[2 * (size_t)t0 + 1]);
   for (uint32_t t = t0 + 1; t <= t1; t++) acc = tail_add(acc, ld_vec(&partials[2 * (size_t)t]));
   st_vec(&buckets[g], acc);
+}
+
+// The buckets the fixup deferred (over 3 .. fix_max chunks): one lane (pair)
+// each, grid-stride over the device-side count.
+template <class C>
+__global__ void __launch_bounds__(128) k_msm_fixup_rest(const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
+                                                        const uint32_t* __restrict__ ctl,
+                                                        const uint32_t* __restrict__ defer,
+                                                        typename C::X* __restrict__ buckets,
+                                                        const typename C::X* __restrict__ partials) {
+  using X = typename C::X;
+  const uint32_t n = __hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t K = chunk_len(off[G], T);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t g = defer[i];
+    const uint32_t t0 = off[g] / K, t1 = (off[g + 1] - 1) / K;
+    X acc = ld_vec(&partials[2 * (size_t)t0 + 1]);
+#pragma unroll 1
+    for (uint32_t t = t0 + 1; t <= t1; t++) acc = tail_add(acc, ld_vec(&partials[2 * (size_t)t]));
+    st_vec(&buckets[g], acc);
+  }
 }
 
 template <class X>
@@ -478,21 +520,43 @@ __device__ __forceinline__ X shfl_xor_point(const X& v, int d) {
   return o;
 }
 
+// All merge levels in ONE launch (round 5; was one launch per level, 8-9
+// per MSM at ~5 us each although they exit at once unless some bucket spans
+// more than fix_max chunks).  ctl[0] = buckets left to the merge (the
+// fixup's count), ctl[1] = the grid barrier's arrivals.  Level l's groups
+// are spread over the grid (grid-stride); the blocks meet at a counting
+// barrier between levels (agent-scope release before arriving, acquire after
+// leaving: the out[] slots of level l are read by other blocks, on other
+// XCDs, at level l + 1).  The grid is small (<= 64 blocks) so it is resident
+// as soon as the other streams' rounds leave it room.
+ZK_DI void merge_grid_barrier(uint32_t* bar, uint32_t target) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    atomicAdd(bar, 1u);
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(2);
+    __threadfence();
+  }
+  __syncthreads();
+}
+
 template <class C>
 __global__ void __launch_bounds__(128) k_msm_merge(const uint32_t* __restrict__ key,
                                                    const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
-                                                   uint32_t fix_max, uint32_t level, const uint32_t* __restrict__ nbig,
+                                                   uint32_t fix_max, uint32_t nlevels, uint32_t* __restrict__ ctl,
                                                    typename C::X* __restrict__ buckets,
-                                                   const typename C::X* __restrict__ in,
-                                                   typename C::X* __restrict__ out) {
+                                                   typename C::X* __restrict__ pa, typename C::X* __restrict__ pb) {
   using X = typename C::X;
-  if (*nbig == 0) return;   // no bucket over fix_max chunks: nothing at any level
+  if (__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;   // nothing at any level
   const uint32_t M = off[G];
   const uint32_t K = chunk_len(M, T);
+  for (uint32_t level = 1; level <= nlevels; level++) {
+  const X* in = (level & 1) ? pa : pb;
+  X* out = (level & 1) ? pb : pa;
   const uint64_t W = (uint64_t)K << (ZK_MERGE_FAN_LOG * level);
   for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;; u += gridDim.x * blockDim.x) {
   const uint64_t s64 = (uint64_t)u * W;
-  if (s64 >= M) return;
+  if (s64 >= M) break;
   const uint32_t s = (uint32_t)s64, e = (uint32_t)min<uint64_t>(s64 + W, M);
   const uint32_t cw = (uint32_t)(W / MSM_MERGE_FAN);
   // the children's open slots of large buckets, in key order
@@ -520,6 +584,8 @@ __global__ void __launch_bounds__(128) k_msm_merge(const uint32_t* __restrict__ 
     else if (off[b] < s) st_vec(&out[2 * (size_t)u], acc);           // open at the start
     else st_vec(&out[2 * (size_t)u + 1], acc);                       // open at the end
   }
+  }
+  if (level < nlevels) merge_grid_barrier(&ctl[1], level * gridDim.x);
   }
 }
 
@@ -557,6 +623,7 @@ ZK_DI SumSpan rowcol_span(const MsmPlan& p, uint32_t b) {
 // (column partials whose column has bit b) or P (all column partials).
 struct QuantSpan {
   uint32_t len, src, bit, shift;   // bit 32: every term
+  uint32_t cnt;                    // terms in the quantity
 };
 ZK_DI QuantSpan quant_span(const MsmPlan& p, uint32_t b) {
   int w = 0;
@@ -564,12 +631,56 @@ ZK_DI QuantSpan quant_span(const MsmPlan& p, uint32_t b) {
   const uint32_t q = b - p.qoff[w];
   const uint32_t kr = p.kr[w], kc = p.kc[w], lsr = p.lsr[w], lsc = p.lsc[w];
   const uint32_t nr = 1u << (kr + lsr), nc = 1u << (kc + lsc);
-  if (q < kr) return {nr, p.rcoff[w], q, lsr};
-  if (q < kr + kc) return {nc, p.rcoff[w] + nr, q - kr, lsc};
-  return {nc, p.rcoff[w] + nr, 32u, 0u};
+  if (q < kr) return {nr, p.rcoff[w], q, lsr, nr / 2};
+  if (q < kr + kc) return {nc, p.rcoff[w] + nr, q - kr, lsc, nc / 2};
+  return {nc, p.rcoff[w] + nr, 32u, 0u, nc};
 }
-ZK_DI bool quant_has(const QuantSpan& s, uint32_t t) {
-  return t < s.len && (s.bit == 32 || ((t >> (s.bit + s.shift)) & 1));
+// The k-th term of the quantity (k < cnt): the k-th partial whose row /
+// column has the bit (exactly half of them), so the loops visit only the
+// terms (round 5: U^C_b, U^D_b took twice the serial steps they needed).
+ZK_DI uint32_t quant_term(const QuantSpan& s, uint32_t k) {
+  if (s.bit == 32) return k;
+  const uint32_t bb = s.bit + s.shift;
+  return ((k >> bb) << (bb + 1)) | (1u << bb) | (k & ((1u << bb) - 1));
+}
+
+template <class X>
+__device__ __forceinline__ X shfl_point(const X& v, int src) {
+  constexpr int NW = sizeof(X) / 4;
+  X o;
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(&v);
+  uint32_t* d = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+  for (int k = 0; k < NW; k++) d[k] = __shfl(s[k], src);
+  return o;
+}
+
+// The wave's 64 lane points summed by lane-quad adds (curve.hpp): the 32
+// sums of lanes l and l + 32 (the caller's last single-lane step) are folded
+// in 5 quad rounds -- 16 adds (quad j: lanes 2j, 2j + 1), then 8, 4, 2, 1 --
+// instead of 5 more single-lane butterfly steps; a quad add issues about a
+// third of a single-lane add's instructions, and these steps are the
+// latency-bound tail of every sum.  The total is in lanes 0-3.
+#ifndef ZK_ROWCOL_QTAIL
+#define ZK_ROWCOL_QTAIL 0
+#endif
+template <class X>
+ZK_DI X wave_tail_quad(const X& v) {
+  const int j = (threadIdx.x & 63) >> 2;
+  X t;
+#pragma unroll 1
+  for (int it = 0; it < 5; it++) {
+    X a, b;
+    if (it == 0) {
+      a = shfl_point(v, 2 * j);
+      b = shfl_point(v, 2 * j + 1);
+    } else {
+      a = t;
+      b = shfl_xor_point(t, 64 >> it);
+    }
+    t = xyzz_add_quad(a, b);
+  }
+  return t;
 }
 
 // Row sums C_hi (2^kc contiguous buckets) and column sums D_lo (2^kr buckets
@@ -585,50 +696,23 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_rowcol(MsmPlan p, co
   const SumSpan sp = rowcol_span(p, b);
   const uint32_t len = sp.len, g0 = sp.g0, stride = sp.stride;
   const uint32_t niter = (len + 63) >> 6;
+  constexpr uint32_t NB = ZK_ROWCOL_QTAIL ? 1 : 6;   // single-lane butterfly steps
   X v;
   xyzz_set_inf(v);
 #pragma unroll 1
-  for (uint32_t it = 0; it < niter + 6; it++) {
+  for (uint32_t it = 0; it < niter + NB; it++) {
     X o;
     if (it < niter) {
       const uint32_t t = it * 64 + lane, g = g0 + t * stride;
       if (t < len && (p.all_valid || off[g + 1] != off[g])) o = ld_vec(&buckets[g]);
       else xyzz_set_inf(o);
     } else {
-      o = shfl_xor_point(v, 1 << (it - niter));
+      o = shfl_xor_point(v, ZK_ROWCOL_QTAIL ? 32 : 1 << (it - niter));
     }
     v = tail_add(v, o);
   }
+  if constexpr (ZK_ROWCOL_QTAIL) v = wave_tail_quad(v);
   if (lane == 0) st_vec(&rc[b], v);
-}
-
-// Quantities U^C_b (rows with bit b), U^D_b (columns with bit b) and P (all
-// columns) of every window, one wave each.
-template <class C>
-__global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_quant(MsmPlan p, const typename C::X* __restrict__ rc,
-                                                                 typename C::X* __restrict__ res) {
-  using X = typename C::X;
-  const uint32_t b = blockIdx.x * MSM_RED_WAVES + (threadIdx.x >> 6);
-  const uint32_t lane = threadIdx.x & 63;
-  if (b >= p.nq) return;
-  const QuantSpan qs = quant_span(p, b);
-  const X* src = rc + qs.src;
-  const uint32_t niter = (qs.len + 63) >> 6;
-  X v;
-  xyzz_set_inf(v);
-#pragma unroll 1
-  for (uint32_t it = 0; it < niter + 6; it++) {
-    X o;
-    if (it < niter) {
-      const uint32_t t = it * 64 + lane;
-      if (quant_has(qs, t)) o = ld_vec(&src[t]);
-      else xyzz_set_inf(o);
-    } else {
-      o = shfl_xor_point(v, 1 << (it - niter));
-    }
-    v = tail_add(v, o);
-  }
-  if (lane == 0) st_vec(&res[b], v);
 }
 
 // ---- lane-quad reductions (xyzz_add_quad) ------------------------------
@@ -713,7 +797,7 @@ __global__ void __launch_bounds__(64 * RW) k_msm_quant_q(MsmPlan p, const typena
   const QuantSpan qs = quant_span(p, b);
   const X* src = rc + qs.src;
   const uint32_t j = threadIdx.x >> 2;
-  const uint32_t niter = (qs.len + NQ - 1) / NQ;
+  const uint32_t niter = (qs.cnt + NQ - 1) / NQ;
   X v;
   xyzz_set_inf(v);
 #pragma unroll 1
@@ -721,9 +805,9 @@ __global__ void __launch_bounds__(64 * RW) k_msm_quant_q(MsmPlan p, const typena
     X term;
     bool have = false;
     if (it < niter) {
-      const uint32_t t = it * NQ + j;
-      have = quant_has(qs, t);
-      if (have) term = ld_vec(&src[t]);
+      const uint32_t k = it * NQ + j;
+      have = k < qs.cnt;
+      if (have) term = ld_vec(&src[quant_term(qs, k)]);
     }
     const X o = quad_sum_step<X, RW>(v, it, niter, xs, have, term);
     v = xyzz_add_quad(v, o);
@@ -741,35 +825,97 @@ ZK_DI XYZZ<Fq2h> ld_pair(const G2X* p) {
   return {{ld_vec(q + 0)}, {ld_vec(q + 2)}, {ld_vec(q + 4)}, {ld_vec(q + 6)}};
 }
 
-__global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_rowcol_pair(MsmPlan p, const uint32_t* __restrict__ off,
-                                                                       const G2X* __restrict__ buckets,
-                                                                       G2X* __restrict__ rc) {
-  const uint32_t b = blockIdx.x * MSM_RED_WAVES + (threadIdx.x >> 6);
-  const uint32_t pr = (threadIdx.x & 63) >> 1;
-  if (b >= p.nrc) return;   // whole waves
+// RW = ZK_ROWCOL_WAVES_G2 waves per sum (RW > 1: one sum per workgroup, the
+// waves' totals folded over LDS as in k_msm_quant_pair; RW = 1: one sum per
+// wave, MSM_RED_WAVES sums per workgroup).
+#ifndef ZK_ROWCOL_WAVES_G2
+#define ZK_ROWCOL_WAVES_G2 1
+#endif
+template <int RW>
+__global__ void __launch_bounds__(64 * (RW > 1 ? RW : MSM_RED_WAVES)) k_msm_rowcol_pair(
+    MsmPlan p, const uint32_t* __restrict__ off, const G2X* __restrict__ buckets, G2X* __restrict__ rc) {
+  __shared__ XYZZ<Fq2h> xs[RW > 1 ? RW : 2];   // [slot][half]
+  constexpr uint32_t NP = 32 * RW, LR = ilog2_c(RW);
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint32_t b = RW > 1 ? blockIdx.x : blockIdx.x * MSM_RED_WAVES + wave;
+  const uint32_t pr = RW > 1 ? threadIdx.x >> 1 : (threadIdx.x & 63) >> 1;
+  if (b >= p.nrc) return;   // whole waves (RW = 1) / workgroups
   const SumSpan sp = rowcol_span(p, b);
   const uint32_t len = sp.len, g0 = sp.g0, stride = sp.stride;
-  const uint32_t niter = (len + 31) >> 5;
+  const uint32_t niter = (len + NP - 1) / NP;
   XYZZ<Fq2h> v;
   xyzz_set_inf(v);
 #pragma unroll 1
-  for (uint32_t it = 0; it < niter + 5; it++) {
+  for (uint32_t it = 0; it < niter + 5 + LR; it++) {
     XYZZ<Fq2h> o;
     if (it < niter) {
-      const uint32_t t = it * 32 + pr, g = g0 + t * stride;
+      const uint32_t t = it * NP + pr, g = g0 + t * stride;
       if (t < len && (p.all_valid || off[g + 1] != off[g])) o = ld_pair(&buckets[g]);
       else xyzz_set_inf(o);
-    } else {
+    } else if (it < niter + 5) {
       o = shfl_xor_point(v, 2 << (it - niter));
+    } else {
+      const uint32_t k = it - niter - 5, m = 1u << k;
+      __syncthreads();   // the previous step's reads are done
+      if ((wave & (2 * m - 1)) == m && (threadIdx.x & 63) < 2) xs[2 * (wave >> (k + 1)) + pair_half()] = v;
+      __syncthreads();
+      if ((wave & (2 * m - 1)) == 0) o = xs[2 * (wave >> (k + 1)) + pair_half()];
+      else xyzz_set_inf(o);
     }
     v = tail_add(v, o);
   }
-  if ((threadIdx.x & 63) < 2) st_pair(&rc[b], v);
+  if ((RW > 1 ? threadIdx.x : threadIdx.x & 63) < 2) st_pair(&rc[b], v);
+}
+
+// G2 quantities on lane pairs over ZK_QUANT_WAVES_G2 waves: pair j of the
+// workgroup folds terms j, j + 32 RW, ..., a 5-step __shfl_xor butterfly
+// (lane distances 2..32 keep each lane's half) combines a wave, then a
+// log2(RW)-step tree over LDS combines the waves.  Round 5: was the lane-quad
+// kernel on the full Fq2 point, which spills (792 B per lane) at one wave
+// per SIMD.
+#ifndef ZK_QUANT_WAVES_G2
+#define ZK_QUANT_WAVES_G2 4
+#endif
+template <int RW>
+__global__ void __launch_bounds__(64 * RW) k_msm_quant_pair(MsmPlan p, const G2X* __restrict__ rc,
+                                                           G2X* __restrict__ res) {
+  __shared__ XYZZ<Fq2h> xs[RW > 1 ? RW : 2];   // [slot][half]
+  constexpr uint32_t NP = 32 * RW;
+  constexpr uint32_t LR = ilog2_c(RW);
+  const uint32_t b = blockIdx.x;
+  if (b >= p.nq) return;   // whole workgroup
+  const QuantSpan qs = quant_span(p, b);
+  const G2X* src = rc + qs.src;
+  const uint32_t j = threadIdx.x >> 1, wave = threadIdx.x >> 6;
+  const uint32_t niter = (qs.cnt + NP - 1) / NP;
+  XYZZ<Fq2h> v;
+  xyzz_set_inf(v);
+#pragma unroll 1
+  for (uint32_t it = 0; it < niter + 5 + LR; it++) {
+    XYZZ<Fq2h> o;
+    if (it < niter) {
+      const uint32_t k = it * NP + j;
+      if (k < qs.cnt) o = ld_pair(&src[quant_term(qs, k)]);
+      else xyzz_set_inf(o);
+    } else if (it < niter + 5) {
+      o = shfl_xor_point(v, 2 << (it - niter));
+    } else {
+      const uint32_t k = it - niter - 5, m = 1u << k;
+      __syncthreads();   // the previous step's reads are done
+      if ((wave & (2 * m - 1)) == m && (threadIdx.x & 63) < 2) xs[2 * (wave >> (k + 1)) + pair_half()] = v;
+      __syncthreads();
+      if ((wave & (2 * m - 1)) == 0) o = xs[2 * (wave >> (k + 1)) + pair_half()];
+      else xyzz_set_inf(o);
+    }
+    v = tail_add(v, o);
+  }
+  if (threadIdx.x < 2) st_pair(&res[b], v);
 }
 
 __global__ void __launch_bounds__(128) k_msm_fixup_pair(const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
                                                         uint32_t fix_max, uint32_t* __restrict__ nbig,
-                                                        G2X* __restrict__ buckets, const G2X* __restrict__ partials) {
+                                                        uint32_t* __restrict__ defer, G2X* __restrict__ buckets,
+                                                        const G2X* __restrict__ partials) {
   const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
   if (g >= G) return;   // pair-uniform from here on
   const uint32_t K = chunk_len(off[G], T);
@@ -781,10 +927,31 @@ __global__ void __launch_bounds__(128) k_msm_fixup_pair(const uint32_t* __restri
     if (!pair_half()) atomicAdd(nbig, 1u);
     return;
   }
+  if (defer) {   // the pair's first lane lists the bucket
+    const bool d = t1 - t0 >= 2;
+    fixup_defer(d && !pair_half(), g, defer, nbig + 2);
+    if (d) return;
+  }
   XYZZ<Fq2h> acc = ld_pair(&partials[2 * (size_t)t0 + 1]);
 #pragma unroll 1
   for (uint32_t t = t0 + 1; t <= t1; t++) acc = tail_add(acc, ld_pair(&partials[2 * (size_t)t]));
   st_pair(&buckets[g], acc);
+}
+__global__ void __launch_bounds__(128) k_msm_fixup_rest_pair(const uint32_t* __restrict__ off, uint32_t G,
+                                                             uint32_t T, const uint32_t* __restrict__ ctl,
+                                                             const uint32_t* __restrict__ defer,
+                                                             G2X* __restrict__ buckets,
+                                                             const G2X* __restrict__ partials) {
+  const uint32_t n = __hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t K = chunk_len(off[G], T);
+  for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 1; i < n; i += gridDim.x * blockDim.x / 2) {
+    const uint32_t g = defer[i];
+    const uint32_t t0 = off[g] / K, t1 = (off[g + 1] - 1) / K;
+    XYZZ<Fq2h> acc = ld_pair(&partials[2 * (size_t)t0 + 1]);
+#pragma unroll 1
+    for (uint32_t t = t0 + 1; t <= t1; t++) acc = tail_add(acc, ld_pair(&partials[2 * (size_t)t]));
+    st_pair(&buckets[g], acc);
+  }
 }
 
 // Two parts of one split MSM (msm_batch_back COMBINE): bucket g = this
@@ -859,7 +1026,7 @@ static uint32_t rowcol_waves() {
     ZK_HIP(hipGetDevice(&dev));
     ZK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     if constexpr (std::is_same<C, G2>::value)
-      ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_rowcol_pair, 64 * MSM_RED_WAVES, 0));
+      ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_rowcol_pair<1>, 64 * MSM_RED_WAVES, 0));
     else
       ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_rowcol<C>, 64 * MSM_RED_WAVES, 0));
     return (uint32_t)std::max(1, per_cu * cus * MSM_RED_WAVES);
@@ -912,6 +1079,19 @@ static void msm_split_sums(MsmPlan& p, uint32_t target, uint32_t lanes) {
   }
 }
 
+// Bucket grouping of the prove path's plans by group.hip's counting passes
+// instead of k_msm_keys + rocPRIM onesweep + k_msm_offsets (ZK_MSM_GROUP=0:
+// A/B build with the sort)
+#ifndef ZK_MSM_GROUP
+#define ZK_MSM_GROUP 0
+#endif
+
+// Accumulate chunks of at least this many entries (0: always one full
+// round of the chip; A/B knob)
+#ifndef ZK_ACCUM_MIN_K
+#define ZK_ACCUM_MIN_K 0
+#endif
+
 // Buckets spread over at most this many accumulate chunks are summed by the
 // serial fixup; larger ones go through the log-depth merge.
 constexpr uint32_t MSM_FIX_MAX = 8;
@@ -934,6 +1114,16 @@ static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hip
   w.key.ensure(sizeof(uint32_t) * (M + ENTQ));
   w.buckets.ensure(sizeof(X) * p.G);
   p.T = accum_threads<C>();
+#if ZK_ACCUM_MIN_K > 0
+  {
+    // at least ZK_ACCUM_MIN_K entries per chunk: fewer chunks (waves per
+    // SIMD) for small MSMs, so their buckets span fewer chunks in the fixup;
+    // whole waves on every SIMD (256 CUs x 4 SIMDs)
+    const uint64_t per_wave = g2 ? 32 : 64, unit = per_wave * 1024;
+    const uint64_t want = ((M + ZK_ACCUM_MIN_K - 1) / ZK_ACCUM_MIN_K + unit - 1) / unit * unit;
+    if (want < p.T) p.T = (uint32_t)std::max<uint64_t>(want, unit);
+  }
+#endif
   p.fix_max = MSM_FIX_MAX;
   // row/column sums: G2 on lane pairs, G1 on lane quads when there are few
   // (ROWCOL_QUAD_MAX, unsplit), else one lane per add, split to fill the chip
@@ -953,13 +1143,18 @@ static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hip
   }
 
   Prof* pf = w.prof;
-  // group the (point, window) entries by bucket: rocPRIM radix sort on
-  // ceil(log2(G + 1)) key bits (log2(G) when shared)
   int ph = pf ? pf->begin(st, (w.tag + "msm_sort").c_str(), n) : -1;
-  unsigned end_bit = 1;
-  while ((1ull << end_bit) < (uint64_t)p.G + (p.shared ? 0 : 1)) end_bit++;
   w.key_in.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
   w.ent_in.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
+  if (ZK_MSM_GROUP && msm_group_ok(p, sw)) {
+    // the prove path's plans: two-level counting grouping (group.hip)
+    msm_group(w, segs, nseg, st);
+    if (pf) pf->end(st, ph);
+  } else {
+  // group the (point, window) entries by bucket: rocPRIM radix sort on
+  // ceil(log2(G + 1)) key bits (log2(G) when shared)
+  unsigned end_bit = 1;
+  while ((1ull << end_bit) < (uint64_t)p.G + (p.shared ? 0 : 1)) end_bit++;
   size_t tmp_bytes = 0;
   sort_pairs_u32(nullptr, tmp_bytes, nullptr, nullptr, nullptr, nullptr, M, end_bit, st);
   w.sort_tmp.ensure(tmp_bytes);
@@ -985,6 +1180,7 @@ static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hip
   k_msm_offsets<<<ceil_div(M + 1, 256), 256, 0, st>>>(w.key.as<uint32_t>(), (uint32_t)M, p.G, w.off.as<uint32_t>());
   ZK_LAUNCH_CHECK();
   if (pf) pf->end(st, ph);
+  }
   // The number of non-zero digits M' <= M is known on device only: the T
   // accumulate threads split it evenly there (chunk_len), no host sync.
   if (M) {
@@ -1013,34 +1209,50 @@ static void msm_back_impl(MsmWork& w, hipStream_t st, int mode, const MsmWork* p
   (void)n;
   const bool quad_rc = p.quad_rc != 0;
   int ph = pf ? pf->begin(st, (w.tag + "msm_merge").c_str(), p.G) : -1;   // buckets split across chunks
-  w.nbig.ensure(sizeof(uint32_t));
-  ZK_HIP(hipMemsetAsync(w.nbig.p, 0, sizeof(uint32_t), st));
+  // ctl: [0] buckets left to the merge, [1] its grid barrier, [2] deferred buckets
+  w.nbig.ensure(3 * sizeof(uint32_t));
+  ZK_HIP(hipMemsetAsync(w.nbig.p, 0, 3 * sizeof(uint32_t), st));
+  // defer the multi-add buckets when buckets mostly span <= 2 chunks (T <= 1.5 G)
+  const bool by_boundary = !g2 && p.G > p.T;
+  const bool defer = ZK_FIXUP_DEFER && !by_boundary && 2ull * p.T <= 3ull * p.G;
+  uint32_t* dlist = nullptr;
+  if (defer) {
+    w.fdefer.ensure(sizeof(uint32_t) * p.G);
+    dlist = w.fdefer.as<uint32_t>();
+  }
   if constexpr (g2)
     k_msm_fixup_pair<<<ceil_div(2 * (size_t)p.G, 128), 128, 0, st>>>(
-        w.off.as<uint32_t>(), p.G, p.T, p.fix_max, w.nbig.as<uint32_t>(), reinterpret_cast<G2X*>(w.buckets.p),
-        reinterpret_cast<const G2X*>(w.partials.p));
+        w.off.as<uint32_t>(), p.G, p.T, p.fix_max, w.nbig.as<uint32_t>(), dlist,
+        reinterpret_cast<G2X*>(w.buckets.p), reinterpret_cast<const G2X*>(w.partials.p));
   else
-  {
-    const bool by_boundary = p.G > p.T;
     k_msm_fixup<C><<<ceil_div(by_boundary ? p.T : p.G, 128), 128, 0, st>>>(
-        w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T, p.fix_max, by_boundary, w.nbig.as<uint32_t>(),
+        w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T, p.fix_max, by_boundary, w.nbig.as<uint32_t>(), dlist,
         w.buckets.as<X>(), w.partials.as<X>());
-  }
   ZK_LAUNCH_CHECK();
+  if (defer) {
+    // a small grid-stride grid: ~4 % of the buckets in the common case
+    if constexpr (g2)
+      k_msm_fixup_rest_pair<<<std::min<uint32_t>(ceil_div(2 * (size_t)p.G, 128), 128), 128, 0, st>>>(
+          w.off.as<uint32_t>(), p.G, p.T, w.nbig.as<uint32_t>(), dlist, reinterpret_cast<G2X*>(w.buckets.p),
+          reinterpret_cast<const G2X*>(w.partials.p));
+    else
+      k_msm_fixup_rest<C><<<std::min<uint32_t>(ceil_div(p.G, 128), 128), 128, 0, st>>>(
+          w.off.as<uint32_t>(), p.G, p.T, w.nbig.as<uint32_t>(), dlist, w.buckets.as<X>(), w.partials.as<X>());
+    ZK_LAUNCH_CHECK();
+  }
   {
-    X* a = w.partials.as<X>();
-    X* b = w.partials2.as<X>();
-    // level l merges groups of FAN^l chunks; T chunks at most
-    for (uint32_t level = 1; (1ull << (ZK_MERGE_FAN_LOG * (level - 1))) < p.T; level++) {
-      const uint32_t groups = (uint32_t)(((uint64_t)p.T + (1ull << (ZK_MERGE_FAN_LOG * level)) - 1) >>
-                                         (ZK_MERGE_FAN_LOG * level));
+    // level l merges groups of FAN^l chunks; T chunks at most.  The levels
+    // ping-pong between partials (level 0 = the chunks) and partials2.
+    uint32_t nlevels = 0;
+    while ((1ull << (ZK_MERGE_FAN_LOG * nlevels)) < p.T) nlevels++;
+    const uint32_t groups1 = (uint32_t)(((uint64_t)p.T + MSM_MERGE_FAN - 1) >> ZK_MERGE_FAN_LOG);
+    if (nlevels) {
       // a small grid-stride grid: the common case exits at once and should
       // not queue hundreds of blocks behind other streams' long kernels
-      k_msm_merge<C><<<std::min<uint32_t>(ceil_div(groups, 128), 64), 128, 0, st>>>(
-          w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T, p.fix_max, level, w.nbig.as<uint32_t>(),
-          w.buckets.as<X>(), a, b);
+      k_msm_merge<C><<<std::min<uint32_t>(ceil_div(groups1, 128), 64), 128, 0, st>>>(
+          w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T, p.fix_max, nlevels, w.nbig.as<uint32_t>(),
+          w.buckets.as<X>(), w.partials.as<X>(), w.partials2.as<X>());
       ZK_LAUNCH_CHECK();
-      std::swap(a, b);
     }
   }
   p.all_valid = 0;
@@ -1062,16 +1274,23 @@ static void msm_back_impl(MsmWork& w, hipStream_t st, int mode, const MsmWork* p
   ph = pf ? pf->begin(st, (w.tag + "msm_bucket_sum").c_str(), p.G) : -1;   // row/col sums + quantities
   constexpr int RW = ZK_RED_QWAVES;
   if constexpr (g2)
-    k_msm_rowcol_pair<<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(
-        p, w.off.as<uint32_t>(), reinterpret_cast<const G2X*>(w.buckets.p), reinterpret_cast<G2X*>(w.rc.p));
+  {
+    constexpr int RW2 = ZK_ROWCOL_WAVES_G2;
+    k_msm_rowcol_pair<RW2><<<RW2 > 1 ? p.nrc : ceil_div(p.nrc, MSM_RED_WAVES), 64 * (RW2 > 1 ? RW2 : MSM_RED_WAVES),
+                             0, st>>>(p, w.off.as<uint32_t>(), reinterpret_cast<const G2X*>(w.buckets.p),
+                                      reinterpret_cast<G2X*>(w.rc.p));
+  }
   else if (quad_rc)
     k_msm_rowcol_q<C, RW><<<p.nrc, 64 * RW, 0, st>>>(p, w.off.as<uint32_t>(), w.buckets.as<X>(), w.rc.as<X>());
   else
     k_msm_rowcol<C><<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.off.as<uint32_t>(),
                                                                                   w.buckets.as<X>(), w.rc.as<X>());
   ZK_LAUNCH_CHECK();
-  constexpr int RWQ = g2 ? ZK_RED_QWAVES : ZK_QUANT_WAVES_G1;
-  k_msm_quant_q<C, RWQ><<<p.nq, 64 * RWQ, 0, st>>>(p, w.rc.as<X>(), w.res.as<X>());
+  if constexpr (g2)
+    k_msm_quant_pair<ZK_QUANT_WAVES_G2><<<p.nq, 64 * ZK_QUANT_WAVES_G2, 0, st>>>(
+        p, reinterpret_cast<const G2X*>(w.rc.p), reinterpret_cast<G2X*>(w.res.p));
+  else
+    k_msm_quant_q<C, ZK_QUANT_WAVES_G1><<<p.nq, 64 * ZK_QUANT_WAVES_G1, 0, st>>>(p, w.rc.as<X>(), w.res.as<X>());
   ZK_LAUNCH_CHECK();
   if (pf) pf->end(st, ph);
 }

@@ -50,6 +50,7 @@ struct G2 {
 };
 
 constexpr int MSM_MAXWIN = 64;
+constexpr uint32_t MSM_DUMMY = 0x7fffffffu;   // entry that contributes nothing (a zero digit)
 
 struct MsmPlan {
   int c, nwin, bits, sw;            // window bits, #windows, scalar bits, u64 words/scalar
@@ -90,6 +91,13 @@ struct MsmSeg {
 };
 
 MsmPlan msm_make_plan(uint32_t n, int bits, int sw, int force_c = 0);
+// Bucket grouping without a general radix sort (group.hip) for shared / batch
+// plans with 16-bit bucket ids and <= 4 windows (every prove MSM at c = 16):
+// fills w.key / w.ent grouped by bucket (any order inside a bucket) and w.off.
+struct MsmWork;
+struct MsmSeg;
+bool msm_group_ok(const MsmPlan& p, int sw);
+void msm_group(MsmWork& w, const MsmSeg* segs, int nseg, hipStream_t st);
 // Window-shared plan: digit window w of point i uses the precomputed base
 // 2^(c w) P_i (msm_precompute_windows), so every window accumulates into
 // ONE set of 2^max(c-1, top) buckets -- the bucket reduction shrinks by the
@@ -100,7 +108,9 @@ MsmPlan msm_make_plan_shared(uint32_t n, int bits, int sw, int c);
 struct MsmWork {
   DevBuf off, ent, key, buckets, partials, partials2, rc, res;
   DevBuf key_in, ent_in, sort_tmp;   // radix-sort input and scratch
-  DevBuf nbig;                       // buckets left to the merge levels
+  DevBuf nbig;                       // merge / fixup control words (msm_back_impl)
+  DevBuf fdefer;                     // buckets the fixup deferred to its second pass
+  DevBuf gcnt, gcnt_off;             // bucket grouping (group.hip): per-tile coarse-bin counts, their scan
   PinnedBuf host_res;
   MsmPlan plan{};
   Prof* prof = nullptr;  // optional live kernel timing

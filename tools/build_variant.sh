@@ -7,7 +7,7 @@ set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 name=$1; rev=${2:--}; shift; shift || true
 out=$R/zero-knowledge-proofs_amd/var_$name
-mkdir -p $out
+mkdir -p $out; rm -rf /tmp/zk_build_$name   # flags are not tracked by make: always a clean build
 if [ "$rev" = "-" ]; then
   src=$R
 else

@@ -432,26 +432,6 @@ __device__ __forceinline__ bool big_bucket(const uint32_t* off, uint32_t b, uint
   return (off[b + 1] - 1) / K - off[b] / K + 1 > fix_max;
 }
 
-// Fixup deferral (ZK_FIXUP_DEFER, plans whose buckets mostly span two
-// chunks): the first pass does only the one-add buckets, so each of its
-// waves runs one add instead of its slowest lane's two or three (~4 % of the
-// buckets span three chunks, but nearly every wave holds one); the others
-// are listed (wave-aggregated atomic) for k_msm_fixup_rest.  Returns whether
-// the lane's bucket was deferred.
-#ifndef ZK_FIXUP_DEFER
-#define ZK_FIXUP_DEFER 0
-#endif
-ZK_DI bool fixup_defer(bool d, uint32_t g, uint32_t* __restrict__ defer, uint32_t* __restrict__ cnt) {
-  const uint64_t m = __ballot(d);
-  if (!m) return false;
-  const int leader = __ffsll((unsigned long long)m) - 1;
-  uint32_t base = 0;
-  if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(cnt, (uint32_t)__popcll(m));
-  base = __shfl(base, leader);
-  if (d) defer[base + __popcll(m & ((1ull << (threadIdx.x & 63)) - 1))] = g;
-  return d;
-}
-
 // One thread per bucket, or -- when there are more buckets than chunks
 // (by_boundary: the 2^19-bucket full-width MSM, where most buckets lie inside
 // one chunk and most per-bucket lanes would idle) one thread per chunk
@@ -460,8 +440,7 @@ ZK_DI bool fixup_defer(bool d, uint32_t g, uint32_t* __restrict__ defer, uint32_
 template <class C>
 __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ key, const uint32_t* __restrict__ off,
                                                    uint32_t G, uint32_t T, uint32_t fix_max, bool by_boundary,
-                                                   uint32_t* __restrict__ nbig, uint32_t* __restrict__ defer,
-                                                   typename C::X* __restrict__ buckets,
+                                                   uint32_t* __restrict__ nbig, typename C::X* __restrict__ buckets,
                                                    const typename C::X* __restrict__ partials) {
   using X = typename C::X;
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
@@ -482,31 +461,9 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
     atomicAdd(nbig, 1u);
     return;
   }
-  if (defer && fixup_defer(t1 - t0 >= 2, g, defer, nbig + 2)) return;
   X acc = ld_vec(&partials[2 * (size_t)t0 + 1]);
   for (uint32_t t = t0 + 1; t <= t1; t++) acc = tail_add(acc, ld_vec(&partials[2 * (size_t)t]));
   st_vec(&buckets[g], acc);
-}
-
-// The buckets the fixup deferred (over 3 .. fix_max chunks): one lane (pair)
-// each, grid-stride over the device-side count.
-template <class C>
-__global__ void __launch_bounds__(128) k_msm_fixup_rest(const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
-                                                        const uint32_t* __restrict__ ctl,
-                                                        const uint32_t* __restrict__ defer,
-                                                        typename C::X* __restrict__ buckets,
-                                                        const typename C::X* __restrict__ partials) {
-  using X = typename C::X;
-  const uint32_t n = __hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t K = chunk_len(off[G], T);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t g = defer[i];
-    const uint32_t t0 = off[g] / K, t1 = (off[g + 1] - 1) / K;
-    X acc = ld_vec(&partials[2 * (size_t)t0 + 1]);
-#pragma unroll 1
-    for (uint32_t t = t0 + 1; t <= t1; t++) acc = tail_add(acc, ld_vec(&partials[2 * (size_t)t]));
-    st_vec(&buckets[g], acc);
-  }
 }
 
 template <class X>
@@ -662,7 +619,7 @@ __device__ __forceinline__ X shfl_point(const X& v, int src) {
 // third of a single-lane add's instructions, and these steps are the
 // latency-bound tail of every sum.  The total is in lanes 0-3.
 #ifndef ZK_ROWCOL_QTAIL
-#define ZK_ROWCOL_QTAIL 0
+#define ZK_ROWCOL_QTAIL 1
 #endif
 template <class X>
 ZK_DI X wave_tail_quad(const X& v) {
@@ -825,46 +782,30 @@ ZK_DI XYZZ<Fq2h> ld_pair(const G2X* p) {
   return {{ld_vec(q + 0)}, {ld_vec(q + 2)}, {ld_vec(q + 4)}, {ld_vec(q + 6)}};
 }
 
-// RW = ZK_ROWCOL_WAVES_G2 waves per sum (RW > 1: one sum per workgroup, the
-// waves' totals folded over LDS as in k_msm_quant_pair; RW = 1: one sum per
-// wave, MSM_RED_WAVES sums per workgroup).
-#ifndef ZK_ROWCOL_WAVES_G2
-#define ZK_ROWCOL_WAVES_G2 1
-#endif
-template <int RW>
-__global__ void __launch_bounds__(64 * (RW > 1 ? RW : MSM_RED_WAVES)) k_msm_rowcol_pair(
-    MsmPlan p, const uint32_t* __restrict__ off, const G2X* __restrict__ buckets, G2X* __restrict__ rc) {
-  __shared__ XYZZ<Fq2h> xs[RW > 1 ? RW : 2];   // [slot][half]
-  constexpr uint32_t NP = 32 * RW, LR = ilog2_c(RW);
-  const uint32_t wave = threadIdx.x >> 6;
-  const uint32_t b = RW > 1 ? blockIdx.x : blockIdx.x * MSM_RED_WAVES + wave;
-  const uint32_t pr = RW > 1 ? threadIdx.x >> 1 : (threadIdx.x & 63) >> 1;
-  if (b >= p.nrc) return;   // whole waves (RW = 1) / workgroups
+__global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_rowcol_pair(MsmPlan p, const uint32_t* __restrict__ off,
+                                                                       const G2X* __restrict__ buckets,
+                                                                       G2X* __restrict__ rc) {
+  const uint32_t b = blockIdx.x * MSM_RED_WAVES + (threadIdx.x >> 6);
+  const uint32_t pr = (threadIdx.x & 63) >> 1;
+  if (b >= p.nrc) return;   // whole waves
   const SumSpan sp = rowcol_span(p, b);
   const uint32_t len = sp.len, g0 = sp.g0, stride = sp.stride;
-  const uint32_t niter = (len + NP - 1) / NP;
+  const uint32_t niter = (len + 31) >> 5;
   XYZZ<Fq2h> v;
   xyzz_set_inf(v);
 #pragma unroll 1
-  for (uint32_t it = 0; it < niter + 5 + LR; it++) {
+  for (uint32_t it = 0; it < niter + 5; it++) {
     XYZZ<Fq2h> o;
     if (it < niter) {
-      const uint32_t t = it * NP + pr, g = g0 + t * stride;
+      const uint32_t t = it * 32 + pr, g = g0 + t * stride;
       if (t < len && (p.all_valid || off[g + 1] != off[g])) o = ld_pair(&buckets[g]);
       else xyzz_set_inf(o);
-    } else if (it < niter + 5) {
-      o = shfl_xor_point(v, 2 << (it - niter));
     } else {
-      const uint32_t k = it - niter - 5, m = 1u << k;
-      __syncthreads();   // the previous step's reads are done
-      if ((wave & (2 * m - 1)) == m && (threadIdx.x & 63) < 2) xs[2 * (wave >> (k + 1)) + pair_half()] = v;
-      __syncthreads();
-      if ((wave & (2 * m - 1)) == 0) o = xs[2 * (wave >> (k + 1)) + pair_half()];
-      else xyzz_set_inf(o);
+      o = shfl_xor_point(v, 2 << (it - niter));
     }
     v = tail_add(v, o);
   }
-  if ((RW > 1 ? threadIdx.x : threadIdx.x & 63) < 2) st_pair(&rc[b], v);
+  if ((threadIdx.x & 63) < 2) st_pair(&rc[b], v);
 }
 
 // G2 quantities on lane pairs over ZK_QUANT_WAVES_G2 waves: pair j of the
@@ -912,13 +853,24 @@ __global__ void __launch_bounds__(64 * RW) k_msm_quant_pair(MsmPlan p, const G2X
   if (threadIdx.x < 2) st_pair(&res[b], v);
 }
 
-__global__ void __launch_bounds__(128) k_msm_fixup_pair(const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
-                                                        uint32_t fix_max, uint32_t* __restrict__ nbig,
-                                                        uint32_t* __restrict__ defer, G2X* __restrict__ buckets,
+// G2 fixup on lane pairs, per bucket or (by_boundary, more buckets than
+// chunks: c = 22 at 2^24, 2^21 buckets over 65 K chunks) per chunk boundary as
+// k_msm_fixup<G1> (round 5; one pair per bucket cost 1.15 ms per 2^24 proof).
+__global__ void __launch_bounds__(128) k_msm_fixup_pair(const uint32_t* __restrict__ key,
+                                                        const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
+                                                        uint32_t fix_max, bool by_boundary,
+                                                        uint32_t* __restrict__ nbig, G2X* __restrict__ buckets,
                                                         const G2X* __restrict__ partials) {
-  const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
-  if (g >= G) return;   // pair-uniform from here on
+  const uint32_t u = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;   // pair-uniform from here on
   const uint32_t K = chunk_len(off[G], T);
+  uint32_t g = u;
+  if (by_boundary) {
+    if (u == 0 || u >= T || (uint64_t)u * K >= off[G]) return;
+    g = key[u * K];
+    if (off[g] / K != u - 1) return;   // not split here, or not its first boundary
+  } else if (g >= G) {
+    return;
+  }
   const uint32_t bs = off[g], be = off[g + 1];
   if (be == bs) return;
   const uint32_t t0 = bs / K, t1 = (be - 1) / K;
@@ -927,31 +879,10 @@ __global__ void __launch_bounds__(128) k_msm_fixup_pair(const uint32_t* __restri
     if (!pair_half()) atomicAdd(nbig, 1u);
     return;
   }
-  if (defer) {   // the pair's first lane lists the bucket
-    const bool d = t1 - t0 >= 2;
-    fixup_defer(d && !pair_half(), g, defer, nbig + 2);
-    if (d) return;
-  }
   XYZZ<Fq2h> acc = ld_pair(&partials[2 * (size_t)t0 + 1]);
 #pragma unroll 1
   for (uint32_t t = t0 + 1; t <= t1; t++) acc = tail_add(acc, ld_pair(&partials[2 * (size_t)t]));
   st_pair(&buckets[g], acc);
-}
-__global__ void __launch_bounds__(128) k_msm_fixup_rest_pair(const uint32_t* __restrict__ off, uint32_t G,
-                                                             uint32_t T, const uint32_t* __restrict__ ctl,
-                                                             const uint32_t* __restrict__ defer,
-                                                             G2X* __restrict__ buckets,
-                                                             const G2X* __restrict__ partials) {
-  const uint32_t n = __hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t K = chunk_len(off[G], T);
-  for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 1; i < n; i += gridDim.x * blockDim.x / 2) {
-    const uint32_t g = defer[i];
-    const uint32_t t0 = off[g] / K, t1 = (off[g + 1] - 1) / K;
-    XYZZ<Fq2h> acc = ld_pair(&partials[2 * (size_t)t0 + 1]);
-#pragma unroll 1
-    for (uint32_t t = t0 + 1; t <= t1; t++) acc = tail_add(acc, ld_pair(&partials[2 * (size_t)t]));
-    st_pair(&buckets[g], acc);
-  }
 }
 
 // Two parts of one split MSM (msm_batch_back COMBINE): bucket g = this
@@ -1026,7 +957,7 @@ static uint32_t rowcol_waves() {
     ZK_HIP(hipGetDevice(&dev));
     ZK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     if constexpr (std::is_same<C, G2>::value)
-      ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_rowcol_pair<1>, 64 * MSM_RED_WAVES, 0));
+      ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_rowcol_pair, 64 * MSM_RED_WAVES, 0));
     else
       ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_rowcol<C>, 64 * MSM_RED_WAVES, 0));
     return (uint32_t)std::max(1, per_cu * cus * MSM_RED_WAVES);
@@ -1086,12 +1017,6 @@ static void msm_split_sums(MsmPlan& p, uint32_t target, uint32_t lanes) {
 #define ZK_MSM_GROUP 0
 #endif
 
-// Accumulate chunks of at least this many entries (0: always one full
-// round of the chip; A/B knob)
-#ifndef ZK_ACCUM_MIN_K
-#define ZK_ACCUM_MIN_K 0
-#endif
-
 // Buckets spread over at most this many accumulate chunks are summed by the
 // serial fixup; larger ones go through the log-depth merge.
 constexpr uint32_t MSM_FIX_MAX = 8;
@@ -1114,16 +1039,6 @@ static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hip
   w.key.ensure(sizeof(uint32_t) * (M + ENTQ));
   w.buckets.ensure(sizeof(X) * p.G);
   p.T = accum_threads<C>();
-#if ZK_ACCUM_MIN_K > 0
-  {
-    // at least ZK_ACCUM_MIN_K entries per chunk: fewer chunks (waves per
-    // SIMD) for small MSMs, so their buckets span fewer chunks in the fixup;
-    // whole waves on every SIMD (256 CUs x 4 SIMDs)
-    const uint64_t per_wave = g2 ? 32 : 64, unit = per_wave * 1024;
-    const uint64_t want = ((M + ZK_ACCUM_MIN_K - 1) / ZK_ACCUM_MIN_K + unit - 1) / unit * unit;
-    if (want < p.T) p.T = (uint32_t)std::max<uint64_t>(want, unit);
-  }
-#endif
   p.fix_max = MSM_FIX_MAX;
   // row/column sums: G2 on lane pairs, G1 on lane quads when there are few
   // (ROWCOL_QUAD_MAX, unsplit), else one lane per add, split to fill the chip
@@ -1181,6 +1096,8 @@ static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hip
   ZK_LAUNCH_CHECK();
   if (pf) pf->end(st, ph);
   }
+  if (w.sorted_ev) ZK_HIP(hipEventRecord(w.sorted_ev, st));
+  if (w.accum_wait) ZK_HIP(hipStreamWaitEvent(st, w.accum_wait, 0));
   // The number of non-zero digits M' <= M is known on device only: the T
   // accumulate threads split it evenly there (chunk_len), no host sync.
   if (M) {
@@ -1209,37 +1126,20 @@ static void msm_back_impl(MsmWork& w, hipStream_t st, int mode, const MsmWork* p
   (void)n;
   const bool quad_rc = p.quad_rc != 0;
   int ph = pf ? pf->begin(st, (w.tag + "msm_merge").c_str(), p.G) : -1;   // buckets split across chunks
-  // ctl: [0] buckets left to the merge, [1] its grid barrier, [2] deferred buckets
-  w.nbig.ensure(3 * sizeof(uint32_t));
-  ZK_HIP(hipMemsetAsync(w.nbig.p, 0, 3 * sizeof(uint32_t), st));
-  // defer the multi-add buckets when buckets mostly span <= 2 chunks (T <= 1.5 G)
-  const bool by_boundary = !g2 && p.G > p.T;
-  const bool defer = ZK_FIXUP_DEFER && !by_boundary && 2ull * p.T <= 3ull * p.G;
-  uint32_t* dlist = nullptr;
-  if (defer) {
-    w.fdefer.ensure(sizeof(uint32_t) * p.G);
-    dlist = w.fdefer.as<uint32_t>();
-  }
+  // ctl: [0] buckets left to the merge, [1] its grid barrier
+  w.nbig.ensure(2 * sizeof(uint32_t));
+  ZK_HIP(hipMemsetAsync(w.nbig.p, 0, 2 * sizeof(uint32_t), st));
+  const bool by_boundary = p.G > p.T;
+  const size_t fix_n = by_boundary ? p.T : p.G;
   if constexpr (g2)
-    k_msm_fixup_pair<<<ceil_div(2 * (size_t)p.G, 128), 128, 0, st>>>(
-        w.off.as<uint32_t>(), p.G, p.T, p.fix_max, w.nbig.as<uint32_t>(), dlist,
+    k_msm_fixup_pair<<<ceil_div(2 * fix_n, 128), 128, 0, st>>>(
+        w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T, p.fix_max, by_boundary, w.nbig.as<uint32_t>(),
         reinterpret_cast<G2X*>(w.buckets.p), reinterpret_cast<const G2X*>(w.partials.p));
   else
-    k_msm_fixup<C><<<ceil_div(by_boundary ? p.T : p.G, 128), 128, 0, st>>>(
-        w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T, p.fix_max, by_boundary, w.nbig.as<uint32_t>(), dlist,
-        w.buckets.as<X>(), w.partials.as<X>());
+    k_msm_fixup<C><<<ceil_div(fix_n, 128), 128, 0, st>>>(w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T,
+                                                          p.fix_max, by_boundary, w.nbig.as<uint32_t>(),
+                                                          w.buckets.as<X>(), w.partials.as<X>());
   ZK_LAUNCH_CHECK();
-  if (defer) {
-    // a small grid-stride grid: ~4 % of the buckets in the common case
-    if constexpr (g2)
-      k_msm_fixup_rest_pair<<<std::min<uint32_t>(ceil_div(2 * (size_t)p.G, 128), 128), 128, 0, st>>>(
-          w.off.as<uint32_t>(), p.G, p.T, w.nbig.as<uint32_t>(), dlist, reinterpret_cast<G2X*>(w.buckets.p),
-          reinterpret_cast<const G2X*>(w.partials.p));
-    else
-      k_msm_fixup_rest<C><<<std::min<uint32_t>(ceil_div(p.G, 128), 128), 128, 0, st>>>(
-          w.off.as<uint32_t>(), p.G, p.T, w.nbig.as<uint32_t>(), dlist, w.buckets.as<X>(), w.partials.as<X>());
-    ZK_LAUNCH_CHECK();
-  }
   {
     // level l merges groups of FAN^l chunks; T chunks at most.  The levels
     // ping-pong between partials (level 0 = the chunks) and partials2.
@@ -1274,12 +1174,8 @@ static void msm_back_impl(MsmWork& w, hipStream_t st, int mode, const MsmWork* p
   ph = pf ? pf->begin(st, (w.tag + "msm_bucket_sum").c_str(), p.G) : -1;   // row/col sums + quantities
   constexpr int RW = ZK_RED_QWAVES;
   if constexpr (g2)
-  {
-    constexpr int RW2 = ZK_ROWCOL_WAVES_G2;
-    k_msm_rowcol_pair<RW2><<<RW2 > 1 ? p.nrc : ceil_div(p.nrc, MSM_RED_WAVES), 64 * (RW2 > 1 ? RW2 : MSM_RED_WAVES),
-                             0, st>>>(p, w.off.as<uint32_t>(), reinterpret_cast<const G2X*>(w.buckets.p),
-                                      reinterpret_cast<G2X*>(w.rc.p));
-  }
+    k_msm_rowcol_pair<<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(
+        p, w.off.as<uint32_t>(), reinterpret_cast<const G2X*>(w.buckets.p), reinterpret_cast<G2X*>(w.rc.p));
   else if (quad_rc)
     k_msm_rowcol_q<C, RW><<<p.nrc, 64 * RW, 0, st>>>(p, w.off.as<uint32_t>(), w.buckets.as<X>(), w.rc.as<X>());
   else

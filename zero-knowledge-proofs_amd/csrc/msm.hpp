@@ -108,13 +108,15 @@ MsmPlan msm_make_plan_shared(uint32_t n, int bits, int sw, int c);
 struct MsmWork {
   DevBuf off, ent, key, buckets, partials, partials2, rc, res;
   DevBuf key_in, ent_in, sort_tmp;   // radix-sort input and scratch
-  DevBuf nbig;                       // merge / fixup control words (msm_back_impl)
-  DevBuf fdefer;                     // buckets the fixup deferred to its second pass
+  DevBuf nbig;                       // merge control words (msm_back_impl)
   DevBuf gcnt, gcnt_off;             // bucket grouping (group.hip): per-tile coarse-bin counts, their scan
   PinnedBuf host_res;
   MsmPlan plan{};
   Prof* prof = nullptr;  // optional live kernel timing
   std::string tag;      // phase-name prefix (per-MSM profiling)
+  // Schedule hooks (not owned; null: none): sorted_ev is recorded once the
+  // entries are grouped, and the accumulate waits for accum_wait first.
+  hipEvent_t sorted_ev = nullptr, accum_wait = nullptr;
 };
 
 // Launch the device part of an MSM over n Montgomery-affine device bases and

@@ -70,7 +70,6 @@ zk_ctx* zk_ctx_create(int device) {
                                          (ZK_SIDE_PRIO_MASK >> i) & 1 ? hi_prio : lo_prio));
     ZK_HIP(hipEventCreateWithFlags(&c->ev_scal, hipEventDisableTiming));
     ZK_HIP(hipEventCreateWithFlags(&c->ev_quot, hipEventDisableTiming));
-    ZK_HIP(hipEventCreateWithFlags(&c->ev_hsorted, hipEventDisableTiming));
     for (auto& e : c->ev_done) ZK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     return c.release();
   } catch (...) {
@@ -88,7 +87,6 @@ void zk_ctx_destroy(zk_ctx* ctx) {
   (void)hipStreamDestroy(ctx->stream);
   (void)hipEventDestroy(ctx->ev_scal);
   (void)hipEventDestroy(ctx->ev_quot);
-  (void)hipEventDestroy(ctx->ev_hsorted);
   for (auto& e : ctx->ev_done) (void)hipEventDestroy(e);
   delete ctx;
 }

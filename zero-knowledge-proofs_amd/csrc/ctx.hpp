@@ -38,7 +38,6 @@ struct zk_ctx {
   hipStream_t side[zk::NUM_SIDE] = {};          // G2 / IC / A+B1 MSM streams
   hipEvent_t ev_scal = nullptr;                 // witness checked (flags reset)
   hipEvent_t ev_quot = nullptr;                 // quotient done (ZK_OPT_EXCHANGE_FIRST)
-  hipEvent_t ev_hsorted = nullptr;              // H entries grouped (quotient-first schedule)
   hipEvent_t ev_done[zk::NUM_MSM] = {};         // per-MSM completion (results downloaded)
   std::string err;
   zk::MsmWork msm[zk::NUM_MSM];

@@ -367,14 +367,6 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_G2_ATTR k_msm_accum_pair(SegBase
   else st_pair(&buckets[cur], acc);
 }
 
-// G1 row/column sums over lane quads when there are at most this many sums:
-// few sums leave most SIMDs idle, so the 4x lanes are free (single-window
-// G1 MSMs, e.g. H: 512 sums)
-#ifndef ZK_ROWCOL_QUAD_MAX
-#define ZK_ROWCOL_QUAD_MAX 600
-#endif
-constexpr uint32_t ROWCOL_QUAD_MAX = ZK_ROWCOL_QUAD_MAX;
-
 // Buckets whose entries span several accumulate chunks.  A bucket over
 // P = t1 - t0 + 1 chunks is tail(t0) + head(t0+1) + ... + head(t1):
 //  * P <= fix_max (the common case: ~1-2): one thread sums the pieces
@@ -678,16 +670,11 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_rowcol(MsmPlan p, co
 // j + 16 RW, ... serially, a 4-step __shfl_xor butterfly (lane distances
 // 4..32 keep each lane's quad position) combines a wave, then a log2(RW)-step
 // tree over LDS combines the waves (wave w + 2^k hands its total to wave w
-// in step k).  One xyzz_add_quad call site.  The quantities (tens of sums)
-// always run on quads, G1 on ZK_QUANT_WAVES_G1 waves per sum (4: one wave per
-// SIMD, 2 terms per quad before the butterfly; round 5: prove 9.173 vs 9.252
-// ms with 8, median of 4 alternating processes, profiles/r05_ab_quant_waves.txt),
-// G2 on ZK_RED_QWAVES (its 456 VGPRs allow one); the
-// G1 row/column sums when there are few of them (ROWCOL_QUAD_MAX), on
-// ZK_RED_QWAVES waves.
-#ifndef ZK_RED_QWAVES
-#define ZK_RED_QWAVES 4
-#endif
+// in step k).  One xyzz_add_quad call site.  The G1 quantities (tens of
+// sums) run on quads, ZK_QUANT_WAVES_G1 waves per sum (4: one wave per SIMD,
+// 2 terms per quad before the butterfly; round 5: prove 9.173 vs 9.252 ms
+// with 8, median of 4 alternating processes, profiles/r05_ab_quant_waves.txt);
+// the G2 ones on lane pairs (k_msm_quant_pair).
 #ifndef ZK_QUANT_WAVES_G1
 #define ZK_QUANT_WAVES_G1 4
 #endif
@@ -711,36 +698,6 @@ __device__ __forceinline__ X quad_sum_step(X v, uint32_t it, uint32_t niter, X* 
     else xyzz_set_inf(o);
   }
   return o;
-}
-
-template <class C, int RW>
-__global__ void __launch_bounds__(64 * RW) k_msm_rowcol_q(MsmPlan p, const uint32_t* __restrict__ off,
-                                                         const typename C::X* __restrict__ buckets,
-                                                         typename C::X* __restrict__ rc) {
-  using X = typename C::X;
-  __shared__ X xs[RW > 1 ? RW / 2 : 1];
-  constexpr uint32_t NQ = 16 * RW;
-  const uint32_t b = blockIdx.x;
-  if (b >= p.nrc) return;   // whole workgroup
-  const SumSpan sp = rowcol_span(p, b);
-  const uint32_t len = sp.len, g0 = sp.g0, stride = sp.stride;
-  const uint32_t j = threadIdx.x >> 2;
-  const uint32_t niter = (len + NQ - 1) / NQ;
-  X v;
-  xyzz_set_inf(v);
-#pragma unroll 1
-  for (uint32_t it = 0; it < niter + 4 + ilog2_c(RW); it++) {
-    X term;
-    bool have = false;
-    if (it < niter) {
-      const uint32_t t = it * NQ + j, g = g0 + t * stride;
-      have = t < len && (p.all_valid || off[g + 1] != off[g]);
-      if (have) term = ld_vec(&buckets[g]);
-    }
-    const X o = quad_sum_step<X, RW>(v, it, niter, xs, have, term);
-    v = xyzz_add_quad(v, o);
-  }
-  if (threadIdx.x == 0) st_vec(&rc[b], v);
 }
 
 template <class C, int RW>
@@ -1040,11 +997,11 @@ static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hip
   w.buckets.ensure(sizeof(X) * p.G);
   p.T = accum_threads<C>();
   p.fix_max = MSM_FIX_MAX;
-  // row/column sums: G2 on lane pairs, G1 on lane quads when there are few
-  // (ROWCOL_QUAD_MAX, unsplit), else one lane per add, split to fill the chip
-  const bool quad_rc = !g2 && p.nrc <= ROWCOL_QUAD_MAX;
-  p.quad_rc = quad_rc;
-  if (!quad_rc && (g2 ? ZK_SPLIT_G2 : ZK_SPLIT_G1)) msm_split_sums(p, rowcol_waves<C>(), g2 ? 32u : 64u);
+  // row/column sums: G2 on lane pairs, G1 one lane per add (lane-quad tail),
+  // split to fill the chip.  Round 5: the H MSM's 512 sums moved from lane
+  // quads (4 waves per sum) to this form, bucket sum 0.285 -> 0.246 ms serial
+  // (profiles/r05_ab_qtail_slowbox.txt)
+  if (g2 ? ZK_SPLIT_G2 : ZK_SPLIT_G1) msm_split_sums(p, rowcol_waves<C>(), g2 ? 32u : 64u);
   w.partials.ensure(sizeof(X) * 2 * (size_t)p.T);
   w.partials2.ensure(sizeof(X) * ((size_t)p.T / 2 + 2));
   w.rc.ensure(sizeof(X) * p.nrc);
@@ -1096,8 +1053,6 @@ static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hip
   ZK_LAUNCH_CHECK();
   if (pf) pf->end(st, ph);
   }
-  if (w.sorted_ev) ZK_HIP(hipEventRecord(w.sorted_ev, st));
-  if (w.accum_wait) ZK_HIP(hipStreamWaitEvent(st, w.accum_wait, 0));
   // The number of non-zero digits M' <= M is known on device only: the T
   // accumulate threads split it evenly there (chunk_len), no host sync.
   if (M) {
@@ -1124,7 +1079,6 @@ static void msm_back_impl(MsmWork& w, hipStream_t st, int mode, const MsmWork* p
   Prof* pf = w.prof;
   const uint32_t n = p.n;
   (void)n;
-  const bool quad_rc = p.quad_rc != 0;
   int ph = pf ? pf->begin(st, (w.tag + "msm_merge").c_str(), p.G) : -1;   // buckets split across chunks
   // ctl: [0] buckets left to the merge, [1] its grid barrier
   w.nbig.ensure(2 * sizeof(uint32_t));
@@ -1172,12 +1126,9 @@ static void msm_back_impl(MsmWork& w, hipStream_t st, int mode, const MsmWork* p
   if (pf) pf->end(st, ph);
   if (mode == MSM_BACK_FIXUP || mode == MSM_BACK_ACCUM) return;
   ph = pf ? pf->begin(st, (w.tag + "msm_bucket_sum").c_str(), p.G) : -1;   // row/col sums + quantities
-  constexpr int RW = ZK_RED_QWAVES;
   if constexpr (g2)
     k_msm_rowcol_pair<<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(
         p, w.off.as<uint32_t>(), reinterpret_cast<const G2X*>(w.buckets.p), reinterpret_cast<G2X*>(w.rc.p));
-  else if (quad_rc)
-    k_msm_rowcol_q<C, RW><<<p.nrc, 64 * RW, 0, st>>>(p, w.off.as<uint32_t>(), w.buckets.as<X>(), w.rc.as<X>());
   else
     k_msm_rowcol<C><<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.off.as<uint32_t>(),
                                                                                   w.buckets.as<X>(), w.rc.as<X>());

@@ -73,7 +73,6 @@ struct MsmPlan {
   int nseg;                         // batch: independent MSMs, reduction window k = MSM k
   uint32_t segshift;                // batch: bucket g belongs to MSM g >> segshift
   int all_valid;                    // every bucket holds a value (msm_batch_back COMBINE wrote them all)
-  int quad_rc;                      // G1 row/column sums on lane quads (few sums, unsplit)
 };
 
 // One MSM of a batch (msm_launch_batch): n points, window-shifted bases
@@ -114,9 +113,6 @@ struct MsmWork {
   MsmPlan plan{};
   Prof* prof = nullptr;  // optional live kernel timing
   std::string tag;      // phase-name prefix (per-MSM profiling)
-  // Schedule hooks (not owned; null: none): sorted_ev is recorded once the
-  // entries are grouped, and the accumulate waits for accum_wait first.
-  hipEvent_t sorted_ev = nullptr, accum_wait = nullptr;
 };
 
 // Launch the device part of an MSM over n Montgomery-affine device bases and

@@ -23,11 +23,6 @@
 #include "dist.hpp"
 #include "quotient.hpp"
 
-// Quotient-first overlapped schedule (A/B build; see prove_device_impl)
-#ifndef ZK_PROVE_QFIRST
-#define ZK_PROVE_QFIRST 0
-#endif
-
 namespace zk {
 
 // ------------------------------------------------------------------ CSR ---
@@ -764,36 +759,13 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   // streams wait for it, so its all-to-alls find free CUs on every rank.
   // (Split uploads are single-GPU only: the quotient needs all of z.)
   const bool xfirst = dist && ctx->exchange_first == 1 && !serial && !split;
-  // Quotient first (ZK_PROVE_QFIRST, A/B build): the quotient alone on the
-  // chip (the G2 / A+B1+IC sorts beside it), then H's sort, then the three
-  // accumulates together -- the G2 and A+B1+IC accumulates wait for H's
-  // entries to be grouped, so no full-occupancy round starves the quotient
-  // or H's sort, and H's tail overlaps the other accumulates.
-  const bool qfirst = ZK_PROVE_QFIRST && !dist && !h_given && !serial && !split;
-  if (qfirst) {
-    run_quotient();
-    ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
-    ctx->msm[MSM_H].sorted_ev = ctx->ev_hsorted;
-    {
-      const int h_slot[1] = {MSM_H};
-      launch_batch(h_slot, 1, "H/", st);
-    }
-    ctx->msm[MSM_H].sorted_ev = nullptr;
-    ctx->msm[MSM_B2].accum_wait = ctx->ev_hsorted;
-    ctx->msm[MSM_A].accum_wait = ctx->ev_hsorted;
-    launch_msms();
-    ctx->msm[MSM_B2].accum_wait = nullptr;
-    ctx->msm[MSM_A].accum_wait = nullptr;
-  }
   if (xfirst) {
     run_quotient();
     ZK_HIP(hipEventRecord(ctx->ev_quot, st));
     ZK_HIP(hipStreamWaitEvent(s_g2, ctx->ev_quot, 0));
     ZK_HIP(hipStreamWaitEvent(s_abi, ctx->ev_quot, 0));
   }
-  if (qfirst) {
-    // enqueued above
-  } else if (split) {
+  if (split) {
     // part k's MSMs, then part k+1 of z (the host thread waits for the
     // pageable copy while the GPU runs the parts already there)
     for (int k = 0; k < HOST_PARTS; k++) {
@@ -810,7 +782,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   } else {
     launch_msms();
   }
-  if (!xfirst && !qfirst) run_quotient();
+  if (!xfirst) run_quotient();
   // the exchange watchdog below counts from here: a host-staged exchange has
   // finished its all-to-alls inside run_quotient, and only local GPU work
   // (RCCL: the enqueued collectives) is left
@@ -821,8 +793,8 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   // ORs of 8 (z_i >= r), 4 / 3 (InvalidWitness) and 2 (division), and the
   // max keeps that precedence.  RCCL: on the stream, no host round trip.
   const bool flags_agreed = dist && ctx->exch->agree_max_dev(ctx->flags.as<uint32_t>(), st);
-  if (!qfirst) {
-    ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
+  ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
+  {
     const int h_slot[1] = {MSM_H};
     launch_batch(h_slot, 1, "H/", st);
   }

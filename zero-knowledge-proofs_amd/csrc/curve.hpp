@@ -265,6 +265,58 @@ ZK_DI XYZZ<F> xyzz_add_quad(const XYZZ<F>& p, const XYZZ<F>& q) {
   return r;
 }
 
+// ---- lane-duo G2 add (latency-bound G2 reductions) ----------------------
+// Four lanes = two lane pairs (units u = 0, 1) hold the same p and q (each
+// lane its Fq2 half, ff.hpp Fq2h) and split every stage's Fq2 products: unit
+// u computes one product of each independent pair, the two interleaved (no
+// scheduling barriers), and the results are broadcast to both units by DPP
+// quad_perm [2K, 2K+1, 2K, 2K+1].  add-2008-s in 4 stages of two products
+// per lane (U1|U2 + S1|S2, PP|RR + ZZ12|ZZZ12, PPP|Q + ZZ3, ZZZ3|R(Q-X3) +
+// S1 PPP) instead of the lane pair's 14 products.  All four lanes must be
+// active and hold the same operands.
+template <int K>
+ZK_DI Fq2h duo_bcast(const Fq2h& v) {
+  Fq2h o;
+#pragma unroll
+  for (int k = 0; k < 12; k++)
+    o.v.v[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.v.v[k], K ? 0xEE : 0x44, 0xf, 0xf, false);
+  return o;
+}
+ZK_DI Fq2h duo_sel(const Fq2h& a0, const Fq2h& a1, uint32_t u) {
+  Fq2h o;
+#pragma unroll
+  for (int k = 0; k < 12; k++) o.v.v[k] = u ? a1.v.v[k] : a0.v.v[k];
+  return o;
+}
+ZK_DI XYZZ<Fq2h> xyzz_add_duo(const XYZZ<Fq2h>& p, const XYZZ<Fq2h>& q) {
+  if (xyzz_is_inf(p)) return q;
+  if (xyzz_is_inf(q)) return p;
+  const uint32_t u = (threadIdx.x >> 1) & 1;
+  Fq2h ma = f_mul(duo_sel(p.X, q.X, u), duo_sel(q.ZZ, p.ZZ, u));     // U1 | U2
+  Fq2h mb = f_mul(duo_sel(p.Y, q.Y, u), duo_sel(q.ZZZ, p.ZZZ, u));   // S1 | S2
+  const Fq2h U1 = duo_bcast<0>(ma), S1 = duo_bcast<0>(mb);
+  const Fq2h P = f_sub(duo_bcast<1>(ma), U1), R = f_sub(duo_bcast<1>(mb), S1);
+  if (f_is_zero(P)) {
+    if (f_is_zero(R)) return xyzz_dbl_call(p);
+    XYZZ<Fq2h> r; xyzz_set_inf(r); return r;
+  }
+  ma = f_sqr(duo_sel(P, R, u));                                          // PP | RR
+  mb = f_mul(duo_sel(p.ZZ, p.ZZZ, u), duo_sel(q.ZZ, q.ZZZ, u));        // ZZ12 | ZZZ12
+  const Fq2h PP = duo_bcast<0>(ma), RR = duo_bcast<1>(ma);
+  const Fq2h ZZ12 = duo_bcast<0>(mb), ZZZ12 = duo_bcast<1>(mb);
+  ma = f_mul(duo_sel(P, U1, u), PP);                                     // PPP | Q
+  mb = f_mul(ZZ12, PP);                                                  // ZZ3 (both units)
+  const Fq2h PPP = duo_bcast<0>(ma), Q = duo_bcast<1>(ma);
+  XYZZ<Fq2h> r;
+  r.ZZ = mb;
+  r.X = f_sub(f_sub(RR, PPP), f_add(Q, Q));
+  ma = f_mul(duo_sel(ZZZ12, R, u), duo_sel(PPP, f_sub(Q, r.X), u));    // ZZZ3 | R (Q - X3)
+  mb = f_mul(S1, PPP);                                                   // S1 PPP (both units)
+  r.ZZZ = duo_bcast<0>(ma);
+  r.Y = f_sub(duo_bcast<1>(ma), mb);
+  return r;
+}
+
 template <class F>
 ZK_DI Affine<F> aff_neg(const Affine<F>& a) { return {a.x, f_neg(a.y)}; }
 

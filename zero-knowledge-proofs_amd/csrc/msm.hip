@@ -739,6 +739,36 @@ ZK_DI XYZZ<Fq2h> ld_pair(const G2X* p) {
   return {{ld_vec(q + 0)}, {ld_vec(q + 2)}, {ld_vec(q + 4)}, {ld_vec(q + 6)}};
 }
 
+// G2 reduction tails on lane duos (curve.hpp xyzz_add_duo: two lane pairs
+// per add, half the pair add's dependent products).  ZK_G2_DUO=0: A/B build
+// with the lane-pair butterflies.
+#ifndef ZK_G2_DUO
+#define ZK_G2_DUO 1
+#endif
+template <int K>
+ZK_DI XYZZ<Fq2h> duo_bcast_point(const XYZZ<Fq2h>& v) {
+  return {duo_bcast<K>(v.X), duo_bcast<K>(v.Y), duo_bcast<K>(v.ZZ), duo_bcast<K>(v.ZZZ)};
+}
+// The wave's 32 lane-pair points summed on duos: duo j first adds pairs 2j
+// and 2j + 1 (its own two pairs), then 8, 4, 2, 1 duo adds across lanes
+// 32 .. 4 apart.  The total is in lanes 0-3.
+ZK_DI XYZZ<Fq2h> wave_tail_duo(const XYZZ<Fq2h>& v) {
+  XYZZ<Fq2h> t;
+#pragma unroll 1
+  for (int it = 0; it < 5; it++) {
+    XYZZ<Fq2h> a, b;
+    if (it == 0) {
+      a = duo_bcast_point<0>(v);
+      b = duo_bcast_point<1>(v);
+    } else {
+      a = t;
+      b = shfl_xor_point(t, 64 >> it);
+    }
+    t = xyzz_add_duo(a, b);
+  }
+  return t;
+}
+
 __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_rowcol_pair(MsmPlan p, const uint32_t* __restrict__ off,
                                                                        const G2X* __restrict__ buckets,
                                                                        G2X* __restrict__ rc) {
@@ -748,10 +778,11 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_rowcol_pair(MsmPlan 
   const SumSpan sp = rowcol_span(p, b);
   const uint32_t len = sp.len, g0 = sp.g0, stride = sp.stride;
   const uint32_t niter = (len + 31) >> 5;
+  constexpr uint32_t NB = ZK_G2_DUO ? 0 : 5;   // lane-pair butterfly steps
   XYZZ<Fq2h> v;
   xyzz_set_inf(v);
 #pragma unroll 1
-  for (uint32_t it = 0; it < niter + 5; it++) {
+  for (uint32_t it = 0; it < niter + NB; it++) {
     XYZZ<Fq2h> o;
     if (it < niter) {
       const uint32_t t = it * 32 + pr, g = g0 + t * stride;
@@ -762,6 +793,7 @@ __global__ void __launch_bounds__(64 * MSM_RED_WAVES) k_msm_rowcol_pair(MsmPlan 
     }
     v = tail_add(v, o);
   }
+  if constexpr (ZK_G2_DUO) v = wave_tail_duo(v);
   if ((threadIdx.x & 63) < 2) st_pair(&rc[b], v);
 }
 
@@ -806,6 +838,45 @@ __global__ void __launch_bounds__(64 * RW) k_msm_quant_pair(MsmPlan p, const G2X
       else xyzz_set_inf(o);
     }
     v = tail_add(v, o);
+  }
+  if (threadIdx.x < 2) st_pair(&res[b], v);
+}
+
+// The G2 quantities on lane duos (ZK_G2_DUO): duo j of the workgroup folds
+// terms j, j + 16 RW, ..., a 4-step __shfl_xor butterfly (lane distances
+// 4 .. 32 keep each lane's duo position), then a log2(RW)-step LDS tree.
+template <int RW>
+__global__ void __launch_bounds__(64 * RW) k_msm_quant_duo(MsmPlan p, const G2X* __restrict__ rc,
+                                                          G2X* __restrict__ res) {
+  __shared__ XYZZ<Fq2h> xs[RW > 1 ? 2 * RW : 4];   // [slot][lane of the duo]
+  constexpr uint32_t NU = 16 * RW;
+  constexpr uint32_t LR = ilog2_c(RW);
+  const uint32_t b = blockIdx.x;
+  if (b >= p.nq) return;   // whole workgroup
+  const QuantSpan qs = quant_span(p, b);
+  const G2X* src = rc + qs.src;
+  const uint32_t j = threadIdx.x >> 2, wave = threadIdx.x >> 6;
+  const uint32_t niter = (qs.cnt + NU - 1) / NU;
+  XYZZ<Fq2h> v;
+  xyzz_set_inf(v);
+#pragma unroll 1
+  for (uint32_t it = 0; it < niter + 4 + LR; it++) {
+    XYZZ<Fq2h> o;
+    if (it < niter) {
+      const uint32_t k = it * NU + j;
+      if (k < qs.cnt) o = ld_pair(&src[quant_term(qs, k)]);
+      else xyzz_set_inf(o);
+    } else if (it < niter + 4) {
+      o = shfl_xor_point(v, 4 << (it - niter));
+    } else {
+      const uint32_t k = it - niter - 4, m = 1u << k;
+      __syncthreads();   // the previous step's reads are done
+      if ((wave & (2 * m - 1)) == m && (threadIdx.x & 63) < 4) xs[4 * (wave >> (k + 1)) + (threadIdx.x & 3)] = v;
+      __syncthreads();
+      if ((wave & (2 * m - 1)) == 0) o = xs[4 * (wave >> (k + 1)) + (threadIdx.x & 3)];
+      else xyzz_set_inf(o);
+    }
+    v = xyzz_add_duo(v, o);
   }
   if (threadIdx.x < 2) st_pair(&res[b], v);
 }
@@ -1133,9 +1204,14 @@ static void msm_back_impl(MsmWork& w, hipStream_t st, int mode, const MsmWork* p
     k_msm_rowcol<C><<<ceil_div(p.nrc, MSM_RED_WAVES), 64 * MSM_RED_WAVES, 0, st>>>(p, w.off.as<uint32_t>(),
                                                                                   w.buckets.as<X>(), w.rc.as<X>());
   ZK_LAUNCH_CHECK();
-  if constexpr (g2)
-    k_msm_quant_pair<ZK_QUANT_WAVES_G2><<<p.nq, 64 * ZK_QUANT_WAVES_G2, 0, st>>>(
-        p, reinterpret_cast<const G2X*>(w.rc.p), reinterpret_cast<G2X*>(w.res.p));
+  if constexpr (g2) {
+    if constexpr (ZK_G2_DUO)
+      k_msm_quant_duo<ZK_QUANT_WAVES_G2><<<p.nq, 64 * ZK_QUANT_WAVES_G2, 0, st>>>(
+          p, reinterpret_cast<const G2X*>(w.rc.p), reinterpret_cast<G2X*>(w.res.p));
+    else
+      k_msm_quant_pair<ZK_QUANT_WAVES_G2><<<p.nq, 64 * ZK_QUANT_WAVES_G2, 0, st>>>(
+          p, reinterpret_cast<const G2X*>(w.rc.p), reinterpret_cast<G2X*>(w.res.p));
+  }
   else
     k_msm_quant_q<C, ZK_QUANT_WAVES_G1><<<p.nq, 64 * ZK_QUANT_WAVES_G1, 0, st>>>(p, w.rc.as<X>(), w.res.as<X>());
   ZK_LAUNCH_CHECK();

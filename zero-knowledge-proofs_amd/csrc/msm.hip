@@ -1039,10 +1039,14 @@ static void msm_split_sums(MsmPlan& p, uint32_t target, uint32_t lanes) {
 }
 
 // Bucket grouping of the prove path's plans by group.hip's counting passes
-// instead of k_msm_keys + rocPRIM onesweep + k_msm_offsets (ZK_MSM_GROUP=0:
-// A/B build with the sort)
+// instead of k_msm_keys + rocPRIM onesweep + k_msm_offsets: 0 never, 1 every
+// plan it takes, 2 (default) single-MSM plans only (G2, H).  Round 5: serial
+// sorts G2 0.136 -> 0.089 ms, H 0.117 -> 0.087 ms; with the A+B1+IC batch as
+// well (1) the overlapped prove lost 0.08-0.15 ms (its grouping kernels hold
+// CU slots the G2 accumulate then lacks), with 2 it is unchanged (9.067 vs
+// 9.040 ms, median of 5, profiles/r05_ab_grouping.txt)
 #ifndef ZK_MSM_GROUP
-#define ZK_MSM_GROUP 0
+#define ZK_MSM_GROUP 2
 #endif
 
 // Buckets spread over at most this many accumulate chunks are summed by the
@@ -1089,7 +1093,7 @@ static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hip
   int ph = pf ? pf->begin(st, (w.tag + "msm_sort").c_str(), n) : -1;
   w.key_in.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
   w.ent_in.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
-  if (ZK_MSM_GROUP && msm_group_ok(p, sw)) {
+  if (ZK_MSM_GROUP && msm_group_ok(p, sw) && (ZK_MSM_GROUP == 1 || nseg == 1)) {
     // the prove path's plans: two-level counting grouping (group.hip)
     msm_group(w, segs, nseg, st);
     if (pf) pf->end(st, ph);

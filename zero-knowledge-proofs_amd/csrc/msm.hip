@@ -1039,14 +1039,17 @@ static void msm_split_sums(MsmPlan& p, uint32_t target, uint32_t lanes) {
 }
 
 // Bucket grouping of the prove path's plans by group.hip's counting passes
-// instead of k_msm_keys + rocPRIM onesweep + k_msm_offsets: 0 never, 1 every
-// plan it takes, 2 (default) single-MSM plans only (G2, H).  Round 5: serial
-// sorts G2 0.136 -> 0.089 ms, H 0.117 -> 0.087 ms; with the A+B1+IC batch as
-// well (1) the overlapped prove lost 0.08-0.15 ms (its grouping kernels hold
-// CU slots the G2 accumulate then lacks), with 2 it is unchanged (9.067 vs
-// 9.040 ms, median of 5, profiles/r05_ab_grouping.txt)
+// instead of k_msm_keys + rocPRIM onesweep + k_msm_offsets: 0 (default)
+// never, 1 every plan it takes, 2 single-MSM plans only (G2, H); A/B builds.
+// Round 5: serial sorts G2 0.136 -> 0.089 ms, H 0.117 -> 0.087 ms; with the
+// A+B1+IC batch as well (1) the overlapped prove lost 0.08-0.15 ms, with 2 it
+// is unchanged (9.067 vs 9.040 ms, median of 5, profiles/r05_ab_grouping.txt).
+// Not the default: the order inside a bucket then follows LDS atomics, so
+// the XYZZ bucket sums -- and the partials zk_groth16_prove_partial returns --
+// differ in their bytes from run to run (the same points; the proof bytes do
+// not change), and the sorted order keeps every partial reproducible.
 #ifndef ZK_MSM_GROUP
-#define ZK_MSM_GROUP 2
+#define ZK_MSM_GROUP 0
 #endif
 
 // Buckets spread over at most this many accumulate chunks are summed by the

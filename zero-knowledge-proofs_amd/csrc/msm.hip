@@ -175,9 +175,12 @@ __global__ void __launch_bounds__(256) k_msm_keys(const uint64_t* __restrict__ s
 }
 
 // off[g] = first sorted position with key >= g, for g in [0, G].
+// ctl (MsmWork::nbig): the merge's control words, zeroed here so that the
+// back phase needs no memset launch of its own.
 __global__ void __launch_bounds__(256) k_msm_offsets(const uint32_t* __restrict__ key, uint32_t M, uint32_t G,
-                                                     uint32_t* __restrict__ off) {
+                                                     uint32_t* __restrict__ off, uint32_t* __restrict__ ctl) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 2) ctl[i] = 0;
   if (i > M) return;
   const uint32_t lo = i ? min(key[i - 1], G) + 1 : 0;     // keys in (key[i-1], key[i]] start at i
   const uint32_t hi = i < M ? min(key[i], G) : G;
@@ -1096,9 +1099,11 @@ static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hip
   int ph = pf ? pf->begin(st, (w.tag + "msm_sort").c_str(), n) : -1;
   w.key_in.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
   w.ent_in.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
+  w.nbig.ensure(2 * sizeof(uint32_t));
   if (ZK_MSM_GROUP && msm_group_ok(p, sw) && (ZK_MSM_GROUP == 1 || nseg == 1)) {
     // the prove path's plans: two-level counting grouping (group.hip)
     msm_group(w, segs, nseg, st);
+    ZK_HIP(hipMemsetAsync(w.nbig.p, 0, 2 * sizeof(uint32_t), st));
     if (pf) pf->end(st, ph);
   } else {
   // group the (point, window) entries by bucket: rocPRIM radix sort on
@@ -1127,7 +1132,8 @@ static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hip
   if (M)
     sort_pairs_u32(w.sort_tmp.p, tmp_bytes, w.key_in.as<uint32_t>(), w.key.as<uint32_t>(), w.ent_in.as<uint32_t>(),
                    w.ent.as<uint32_t>(), M, end_bit, st);
-  k_msm_offsets<<<ceil_div(M + 1, 256), 256, 0, st>>>(w.key.as<uint32_t>(), (uint32_t)M, p.G, w.off.as<uint32_t>());
+  k_msm_offsets<<<ceil_div(M + 1, 256), 256, 0, st>>>(w.key.as<uint32_t>(), (uint32_t)M, p.G, w.off.as<uint32_t>(),
+                                                      w.nbig.as<uint32_t>());
   ZK_LAUNCH_CHECK();
   if (pf) pf->end(st, ph);
   }
@@ -1158,9 +1164,8 @@ static void msm_back_impl(MsmWork& w, hipStream_t st, int mode, const MsmWork* p
   const uint32_t n = p.n;
   (void)n;
   int ph = pf ? pf->begin(st, (w.tag + "msm_merge").c_str(), p.G) : -1;   // buckets split across chunks
-  // ctl: [0] buckets left to the merge, [1] its grid barrier
-  w.nbig.ensure(2 * sizeof(uint32_t));
-  ZK_HIP(hipMemsetAsync(w.nbig.p, 0, 2 * sizeof(uint32_t), st));
+  // ctl (w.nbig, zeroed by the front's k_msm_offsets / grouping): [0]
+  // buckets left to the merge, [1] its grid barrier
   const bool by_boundary = p.G > p.T;
   const size_t fix_n = by_boundary ? p.T : p.G;
   if constexpr (g2)

@@ -2,7 +2,8 @@
 offsets from each prove's first event (zk_ctx_profile(ctx, 2) +
 zk_ctx_timeline_read).
 
-  python tools/timeline_live.py [log_n] [schedule]
+  python tools/timeline_live.py [log_n] [schedule] [host]
+host: the drop-in zk_groth16_prove from a host witness (the split upload)
 """
 import importlib
 import os
@@ -25,12 +26,22 @@ def main():
     qap = zkp.QAP(zkp.CSRMatrices.synthetic(n))
     dpk = zkp.CRS.generate_device(ctx, qap, zkp.SetupParams(*params), 1)
     z = ctx.synthetic_witness(n, 2)
+    host = len(sys.argv) > 3 and sys.argv[3] == "host"
+    if host:
+        import numpy as np
+        w = zkp.Witness(z.cpu().numpy().view(np.uint64), 1)
+
+    def one():
+        if host:
+            zkp.Prover.prove(dpk, w, r=r, s=s)
+        else:
+            zkp.Prover.prove_device(dpk, z.data_ptr(), 3 * n + 1, 1, r, s)
     for _ in range(3):
-        zkp.Prover.prove_device(dpk, z.data_ptr(), 3 * n + 1, 1, r, s)
+        one()
     torch.cuda.synchronize()
     ctx.profile(2)
     for _ in range(4):
-        zkp.Prover.prove_device(dpk, z.data_ptr(), 3 * n + 1, 1, r, s)
+        one()
     text = ctx.timeline_read()
     ctx.profile(False)
     blocks = [b for b in text.strip().split("--") if b.strip()]

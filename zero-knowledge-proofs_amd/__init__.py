@@ -185,7 +185,13 @@ def lib():
         L.zk_last_error.argtypes = [C.c_void_p]
         L.zk_build_id.restype = C.c_char_p
         for name in EXPORTS:
-            f = getattr(L, name)
+            # an A/B build of an older revision (ZK_AMD_LIB, tooling only) may
+            # lack entry points added since; the product library must have all
+            f = getattr(L, name, None)
+            if f is None:
+                if os.environ.get("ZK_AMD_LIB"):
+                    continue
+                raise ImportError(f"{LIB_PATH} does not export {name}")
             if name not in ("zk_ctx_create", "zk_ctx_destroy", "zk_last_error",
                             "zk_msm_bases_free", "zk_pk_free", "zk_build_id"):
                 f.restype = C.c_int

@@ -447,6 +447,67 @@ def anchor_bench(zkp, ctx, log_n, params, r, s, seed, steps, warmup, win_c=0):
                     "/ msm_only.ms_per_step of the N line (DESIGN.md 5)"}
 
 
+def msm_phase_split(prof, steps):
+    """Per-proof ms of the MSM phases of a serial-schedule profile, summed
+    over the MSMs: sort (grouping), accumulate (G1 / G2), merge (fixups),
+    bucket sums (row/column sums + quantities)."""
+    out = {"sort": 0.0, "accum_g1": 0.0, "accum_g2": 0.0, "merge": 0.0, "bucket_sum": 0.0}
+    for k, v in prof.items():
+        ph = k.split("/")[-1]
+        key = {"msm_sort": "sort", "msm_accum_g1": "accum_g1", "msm_accum_g2": "accum_g2", "msm_merge": "merge",
+               "msm_bucket_sum": "bucket_sum"}.get(ph)
+        if key:
+            out[key] += v["ms"] / steps
+    return {k: round(v, 3) for k, v in out.items()}
+
+
+def shard_msm_bench(zkp, ctx, log_n, nshards, params, r, s, seed, ks, anchor_msm_ms, anchor_hex):
+    """One GPU, one shard at a time: the N = nshards lines' key shards of the
+    2^log_n circuit (GPU setup of shard k of nshards, the same witness, r, s
+    as the anchor), each proved with every kernel in order on one stream
+    (zk_ctx_set_schedule 3) and the MSM kernels' HIP-event time taken per
+    proof -- the per-rank MSM work of the N = nshards run, measured here.
+    The shards' partials are folded (zk_groth16_prove_combine) and the proof
+    checked against the anchor's (= the pinned oracle proof).  No exchange is
+    attached, so each shard computes the whole quotient locally; only MSM
+    kernels are counted."""
+    import torch
+    n = 1 << log_n
+    zlen = 3 * n + 1
+    qap = zkp.QAP(zkp.CSRMatrices.synthetic(n))
+    d_z = ctx.synthetic_witness(n, seed + 1)
+    per, parts, phases = [], [], []
+    t0 = time.perf_counter()
+    for k in range(nshards):
+        dpk = zkp.CRS.generate_device(ctx, qap, zkp.SetupParams(*params), 1, shard=k, nshards=nshards)
+        try:
+            ctx.set_schedule(3)
+            part = zkp.Prover.prove_partial(dpk, d_z.data_ptr(), zlen, 1, r, s)   # warm-up, and the partial
+            torch.cuda.synchronize()
+            ctx.profile(True)
+            for _ in range(ks):
+                if zkp.Prover.prove_partial(dpk, d_z.data_ptr(), zlen, 1, r, s) != part:
+                    raise SystemExit(f"shard {k}: partials of consecutive proofs differ")
+            torch.cuda.synchronize()
+            prof = ctx.profile_read()
+        finally:
+            ctx.profile(False)
+            ctx.set_schedule(0)
+            dpk.free()
+        per.append(round(msm_kernel_ms(prof) / ks, 3))
+        phases.append(msm_phase_split(prof, ks))
+        parts.append(part)
+    del d_z
+    proof = zkp.Prover.combine(parts, r, s)
+    worst = max(range(nshards), key=lambda k: per[k])
+    return {"shards": nshards, "constraints_per_shard": n // nshards, "steps": ks,
+            "ms_per_step": per[worst], "shard0_ms": per[0], "slowest_shard": worst, "per_shard_ms": per,
+            "phases_ms_slowest": phases[worst],
+            "msm_scaling_projected": round(anchor_msm_ms / per[worst], 3),
+            "folded_proof_bit_exact_vs_anchor": proof.serialize_compressed().hex() == anchor_hex,
+            "partials_reproducible": True, "wall_s": round(time.perf_counter() - t0, 1)}
+
+
 FR_MUL_MADS = 9 * 9 * 2   # radix-2^29 Fr product: 81 limb products + 81 in the reduction (ff.hpp)
 
 
@@ -693,6 +754,51 @@ def ntt_bench(zkp, ctx, log_n, steps, warmup, seed, cpu=True):
     return rec
 
 
+# The driver keeps only the last ~8 KB of stdout, so the JSON line stays
+# under LINE_BUDGET bytes: the full record (phase tables, notes, long sample
+# descriptions) goes to a file named in the line (`details`), and the line
+# keeps every number (values, rooflines, CPU legs, anchor and shard timings,
+# bit-exactness flags).
+LINE_BUDGET = 6000
+VERBOSE_KEYS = ("phases_ms_total", "note", "timing", "cores_note", "kernel_timing", "event_timing", "api",
+                "schedule", "oracle_reference", "label", "basis", "count", "parity", "bases", "phase_ms",
+                "per_shard_ms")
+
+
+def compact_line(rec, details_path):
+    """Write the full record to details_path and return the compact line."""
+    try:
+        os.makedirs(os.path.dirname(details_path), exist_ok=True)
+        with open(details_path, "w") as f:
+            json.dump(rec, f, indent=1)
+        where = os.path.relpath(details_path, ROOT)
+    except OSError as e:
+        where = f"(not written: {e})"
+
+    def strip(o, depth=0):
+        if isinstance(o, dict):
+            return {k: strip(v, depth + 1) for k, v in o.items()
+                    if k not in VERBOSE_KEYS and not (k == "sample" and isinstance(v, str) and len(v) > 90)}
+        return o
+    line = strip(rec)
+    line["details"] = where
+    # last resort: drop the least important sub-records (all still in the
+    # details file) until the line fits
+    for path in (("strong_scaling_anchor", "same_plan_c16", "serial_schedule"),
+                 ("strong_scaling_anchor", "serial_schedule"), ("serial_schedule",),
+                 ("strong_scaling_anchor", "roofline"), ("msm_g1", "plain"), ("msm_g1", "bits64"),
+                 ("strong_scaling_anchor", "same_plan_c16"), ("ntt", "cpu_baseline"),
+                 ("msm_g1", "cpu_baseline")):
+        if len(json.dumps(line)) <= LINE_BUDGET:
+            break
+        holder = line
+        for k in path[:-1]:
+            holder = holder.get(k) if isinstance(holder, dict) else None
+        if isinstance(holder, dict):
+            holder.pop(path[-1], None)
+    return line
+
+
 def spawn_ranks(n):
     """`--gpus N` without torchrun: start the N ranks as fresh child processes
     (this process has not imported torch or the package and never touches a
@@ -764,6 +870,10 @@ def main():
                     help="N > 1: size of the all-threads oracle sample on rank 0")
     ap.add_argument("--anchor-log-n", type=int, default=24,
                     help="N = 1: the strong-scaling anchor (the N > 1 lines' circuit on one GPU); 0 = skip")
+    ap.add_argument("--shard-scaling", type=int, default=8,
+                    help="N = 1: measure the anchor key's N shards one by one on this GPU (MSM scaling); <2 = skip")
+    ap.add_argument("--details", default=os.path.join(ROOT, "profiles", "bench_details_last.json"),
+                    help="rank 0 writes the full record (phase tables, notes) here; stdout gets the compact line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-msm", action="store_true", help="skip the configs[1] MSM and configs[2] NTT lines")
     ap.add_argument("--no-serial", action="store_true", help="skip the serial-schedule roofline proves")
@@ -834,13 +944,16 @@ def main():
                 ctx.attach_rccl(obj[0][0], rank, world)
             _, err = probe(dist, attach)
             if err:
-                ctx.detach_exchange()
+                probe(dist, ctx.detach_exchange)   # every rank drops it, agreed on the control group
                 quotient_mode = f"replicated (rccl: {err})"
                 log(f"[bench] RCCL attach failed ({err}): replicated quotient")
             else:
                 quotient_mode = "distributed-rccl"
         else:
-            ctx.attach_exchange(zkp.TorchExchange(), rank, world)
+            # the host-staged exchange gets a gloo group of its own: its abort
+            # (a rank failing mid-quotient) destroys that group, never the
+            # control group the fallback below is agreed on
+            ctx.attach_exchange(zkp.TorchExchange(dist.new_group(backend="gloo")), rank, world)
             quotient_mode = "distributed-host"
         if backend == "nccl":
             # the partials' all-gather over RCCL (a torch nccl group beside
@@ -906,10 +1019,15 @@ def main():
     if dist:
         # the first sharded proof, agreed: a distributed quotient that fails
         # on any rank (RCCL between real peers) -> every rank detaches and
-        # carries on with the replicated quotient, labelled
+        # carries on with the replicated quotient, labelled.
+        # ZK_BENCH_FAIL_FIRST_PROOF=k (rehearsal): rank k's first distributed
+        # proof fails after its 2nd all-to-all (test library fault hook)
+        fail_first = int(os.environ.get("ZK_BENCH_FAIL_FIRST_PROOF", "-1"))
+        if fail_first == rank and quotient_mode.startswith("distributed"):
+            ctx.test_fault_after_exchange(2)
         _, err = probe(dist, lambda: zkp.Prover.prove_partial(dpk, d_z.data_ptr(), zlen, 1, r, s))
         if err and quotient_mode.startswith("distributed"):
-            ctx.detach_exchange()
+            probe(dist, ctx.detach_exchange)
             quotient_mode = f"replicated ({quotient_mode.split('-')[1]}: first distributed proof failed: {err})"
             log(f"[bench] first distributed proof failed ({err}): replicated quotient")
             _, err = probe(dist, lambda: zkp.Prover.prove_partial(dpk, d_z.data_ptr(), zlen, 1, r, s))
@@ -1120,6 +1238,15 @@ def main():
                                    1, win_c=16)
                 anc["same_plan_c16"] = {k: c16[k] for k in ("ms_per_step", "value", "msm_only", "window_bits",
                                                             "bit_exact_vs_oracle", "serial_schedule")}
+            if args.shard_scaling > 1:
+                # the N = shard_scaling run's per-rank MSM work, measured on
+                # this GPU shard by shard (north_star's >= 6x MSM scaling)
+                log(f"[bench] the 2^{args.anchor_log_n} key's {args.shard_scaling} shards, one at a time")
+                torch.cuda.empty_cache()
+                sh = shard_msm_bench(zkp, ctx, args.anchor_log_n, args.shard_scaling, params, r, s, args.seed,
+                                     max(2, args.steps // 4), anc["msm_only"]["ms_per_step"], anc["proof_compressed"])
+                anc[f"shard{args.shard_scaling}_msm_only"] = sh
+                anc[f"msm_scaling_projected_{args.shard_scaling}"] = sh["msm_scaling_projected"]
             extra["strong_scaling_anchor"] = anc
     if rank == 0:
         if world == 1:
@@ -1159,7 +1286,8 @@ def main():
             proj["gpu_over_projection"] = round(rec["value"] / proj["value"], 2)
         if world > 1 and log_n_total == 24 and args.seed == DEFAULT_SEED:
             rec["bit_exact_vs_oracle"] = rec["proof_compressed"] == ORACLE_2P24   # the pinned oracle proof
-        sys.stdout.write(json.dumps(rec) + "\n")   # one write: ranks share the launcher's stdout
+        line = compact_line(rec, args.details)
+        sys.stdout.write(json.dumps(line) + "\n")   # one write: ranks share the launcher's stdout
         sys.stdout.flush()
     ctx.close()
     if dist:

@@ -102,3 +102,18 @@ def test_bench_rccl_attach_failure_falls_back_to_replicated(ctx, zkp):
     assert rec["config"]["parallelism"] == "msm-shard2"
     assert "quotient_replicated" not in rec and rec["msm_only"]["ms_per_step"] > 0
     assert rec["proof_compressed"] == _single_gpu_proof(ctx, zkp)
+
+
+@pytest.mark.timeout(300)
+def test_bench_first_distributed_proof_failure_falls_back(ctx, zkp):
+    """ZK_BENCH_FAIL_FIRST_PROOF=1 (gloo, host-staged exchange): rank 1's
+    first distributed proof fails after its 2nd all-to-all, and its abort
+    tears down the exchange's OWN gloo group.  The control group survives,
+    so every rank agrees, detaches (without calling the abort hook again)
+    and carries on with the replicated quotient: the line still comes out,
+    labelled, with the same proof."""
+    rec = _run("bench.py", ZK_BENCH_FAIL_FIRST_PROOF="1")
+    q = rec["config"]["quotient"]
+    assert q.startswith("replicated (host: first distributed proof failed: rank"), q
+    assert "quotient_replicated" not in rec and rec["msm_only"]["ms_per_step"] > 0
+    assert rec["proof_compressed"] == _single_gpu_proof(ctx, zkp)

@@ -539,9 +539,13 @@ int zk_ctx_detach_exchange(zk_ctx* ctx) {
   if (!ctx) return ZK_ERR_ARG;
   ZK_GUARD(ctx, {
     if (ctx->exch) {
-      ZK_HIP(hipStreamSynchronize(ctx->stream));
-      ctx->exch->abort();   // local: the peers detach too, nobody waits for a collective
+      // the exchange is dropped whatever the stream's state: after a GPU
+      // fault (a likely reason to detach) the wait fails, and keeping the
+      // exchange would leave this rank's peers to meet it in a collective
+      const hipError_t e = hipStreamSynchronize(ctx->stream);
+      ctx->exch->detach();
       ctx->exch.reset();
+      if (e != hipSuccess) throw Error(ZK_ERR_DEVICE, std::string("detach: stream wait: ") + hipGetErrorString(e));
     }
     return ZK_OK;
   })

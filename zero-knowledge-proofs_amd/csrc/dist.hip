@@ -407,6 +407,7 @@ struct HostExchange : Exchange {
   void abort() override {
     if (ops.abort) ops.abort(ops.user);
   }
+  void detach() override {}
 };
 
 std::unique_ptr<Exchange> make_host_exchange(const zk_exchange_ops& ops, int rank, int world) {

@@ -48,6 +48,12 @@ struct Exchange {
   // make the peers' pending collectives with this rank fail instead of
   // waiting forever (RCCL: ncclCommAbort; host: the caller's abort callback)
   virtual void abort() = 0;
+  // zk_ctx_detach_exchange: what dropping this exchange must do first.  RCCL
+  // aborts its communicator (local, so no rank waits in a collective for a
+  // rank that left); a host-staged exchange does nothing -- its abort hook
+  // belongs to the caller's transport (TorchExchange destroys a process
+  // group), and a broken one has had its abort already
+  virtual void detach() { abort(); }
   // an asynchronous transport error is pending (RCCL: ncclCommGetAsyncError)
   virtual bool async_error() { return false; }
   // watchdog for waits on work that depends on the peers: give up (throw

@@ -479,17 +479,24 @@ __device__ __forceinline__ X shfl_xor_point(const X& v, int d) {
 // are spread over the grid (grid-stride); the blocks meet at a counting
 // barrier between levels (agent-scope release before arriving, acquire after
 // leaving: the out[] slots of level l are read by other blocks, on other
-// XCDs, at level l + 1).  The grid is small (<= 64 blocks) so it is resident
-// as soon as the other streams' rounds leave it room.
+// XCDs, at level l + 1).
+// Forward progress without a cooperative launch: the grid is capped on the
+// host (msm_back_impl) at min(64, the blocks of this kernel the chip holds at
+// once), so every block fits on the device together; a block waiting at the
+// barrier holds only its own slot, and nothing any other kernel waits on
+// depends on this one, so the other streams' kernels retire and the blocks
+// not yet placed are dispatched -- co-residency is reached, not assumed.
+// The wait costs latency only when the merge runs at all (ctl[0] > 0:
+// skewed scalars).
 ZK_DI void merge_grid_barrier(uint32_t* bar, uint32_t target) {
+  __threadfence();   // every thread's out[] stores, device-wide, before its block arrives
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
-    atomicAdd(bar, 1u);
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(2);
-    __threadfence();
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(2);
   }
   __syncthreads();
+  __threadfence();   // acquire for every thread: the next level reads other blocks' slots
 }
 
 template <class C>
@@ -979,6 +986,20 @@ static uint32_t accum_threads() {
   return T;
 }
 
+// Blocks of the merge kernel the chip holds at once (its occupancy x CUs):
+// the upper bound of its grid-barrier launch.
+template <class C>
+static uint32_t merge_max_blocks() {
+  static const uint32_t B = [] {
+    int dev = 0, cus = 0, per_cu = 0;
+    ZK_HIP(hipGetDevice(&dev));
+    ZK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_msm_merge<C>, 128, 0));
+    return (uint32_t)std::max(0, per_cu * cus);
+  }();
+  return B;
+}
+
 // Waves of one row/column-sum launch that the chip holds at once (the
 // kernel's occupancy x CUs), for msm_split_sums.
 template <class C>
@@ -1185,8 +1206,11 @@ static void msm_back_impl(MsmWork& w, hipStream_t st, int mode, const MsmWork* p
     const uint32_t groups1 = (uint32_t)(((uint64_t)p.T + MSM_MERGE_FAN - 1) >> ZK_MERGE_FAN_LOG);
     if (nlevels) {
       // a small grid-stride grid: the common case exits at once and should
-      // not queue hundreds of blocks behind other streams' long kernels
-      k_msm_merge<C><<<std::min<uint32_t>(ceil_div(groups1, 128), 64), 128, 0, st>>>(
+      // not queue hundreds of blocks behind other streams' long kernels; at
+      // most the blocks the chip holds at once (the grid barrier's bound)
+      const uint32_t grid = std::min<uint32_t>(std::min<uint32_t>(ceil_div(groups1, 128), 64), merge_max_blocks<C>());
+      if (grid < 1 || grid > merge_max_blocks<C>()) throw Error(ZK_ERR_DEVICE, "msm: merge grid exceeds residency");
+      k_msm_merge<C><<<grid, 128, 0, st>>>(
           w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T, p.fix_max, nlevels, w.nbig.as<uint32_t>(),
           w.buckets.as<X>(), w.partials.as<X>(), w.partials2.as<X>());
       ZK_LAUNCH_CHECK();

@@ -956,7 +956,9 @@ static int prove_partial_common(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_
   // all-reduce of {any rank distributed, 2 status + any rank replicated}.
   // A failure after the agreement -- a transport error, a device error, a
   // peer that stopped answering -- aborts the exchange, so the peers'
-  // pending transfers fail too, and marks it dead.
+  // pending transfers fail too, and marks it dead.  A replicated proof after
+  // the agreement uses no exchange: its failures leave the exchange alone.
+  bool in_exchange = true;
   try {
     if (local == ZK_OK && dist) {
       try {
@@ -978,12 +980,15 @@ static int prove_partial_common(zk_ctx* ctx, const zk_pk_dev* pk, const void* d_
     if (local != ZK_OK) {
       p.status = local;
     } else {
+      in_exchange = dist;
       upload();
       p = prove_partial(ctx, pk, reinterpret_cast<const uint64_t*>(d_z), r, s, nullptr, 0, ranges);
     }
   } catch (...) {
-    ctx->exch->broken = true;
-    ctx->exch->abort();
+    if (in_exchange) {
+      ctx->exch->broken = true;
+      ctx->exch->abort();
+    }
     throw;
   }
   std::memcpy(out->bytes, &p, sizeof p);

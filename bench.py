@@ -154,18 +154,18 @@ def traffic_for(log_n):
 
 def msm_kernel_ms(prof):
     """Device ms of the MSM kernels (sort, accumulate, merge, bucket sums) in
-    a profile; serial runs tag phases per MSM ("ABI/msm_accum_g1")."""
+    a profile; serial runs tag phases per MSM pipeline ("AB/msm_accum_g1")."""
     return sum(v["ms"] for k, v in prof.items() if k.split("/")[-1].startswith("msm_"))
 
 
 def roofline_from(prof, log_n, overlapped=None, nshards=1):
     """Dominant kernel: k_msm_accum<G1> (bucket accumulation of the G1 MSMs:
-    the A+B1+IC batch and H), priced at SURVEY 8(d)'s 128 B per scalar-point
-    pair.  `prof` comes from proves run with every kernel in order on one
+    the A+B1 batch and the IC+H MSM), priced at SURVEY 8(d)'s 128 B per
+    scalar-point pair.  `prof` comes from proves run with every kernel in order on one
     stream (zk_ctx_set_schedule 3), so a launch's HIP-event span is the
     kernel's own duration; `overlapped` (a profiled pass of the default
     four-stream schedule, after the timed region) is reported beside it."""
-    def accum(pr):   # serial runs tag phases per MSM ("ABI/msm_accum_g1", "H/msm_accum_g1")
+    def accum(pr):   # serial runs tag phases per MSM pipeline ("AB/msm_accum_g1", "ICH/msm_accum_g1")
         ms = launches = units = 0
         for k, v in pr.items():
             if k.split("/")[-1] == "msm_accum_g1":
@@ -953,7 +953,11 @@ def main():
             # the host-staged exchange gets a gloo group of its own: its abort
             # (a rank failing mid-quotient) destroys that group, never the
             # control group the fallback below is agreed on
-            ctx.attach_exchange(zkp.TorchExchange(dist.new_group(backend="gloo")), rank, world)
+            # (bounded timeout: a peer whose exchange aborted leaves this
+            # rank's pending all-to-all to fail within it, not after the
+            # control group's 900 s)
+            ctx.attach_exchange(zkp.TorchExchange(dist.new_group(backend="gloo", timeout=timedelta(seconds=60))),
+                                rank, world)
             quotient_mode = "distributed-host"
         if backend == "nccl":
             # the partials' all-gather over RCCL (a torch nccl group beside

@@ -10,7 +10,7 @@ for i in $(seq $rounds); do
   for v in base "$@"; do
     lib=""; [ $v != base ] && lib=$PWD/zero-knowledge-proofs_amd/var_$v/libzkp_amd.so
     ZK_AMD_LIB=$lib timeout -k 10 150 python -u bench.py --no-cpu-baseline --no-msm --no-pcie --anchor-log-n 0 \
-      --steps 20 --warmup 5 > gpurun_out/abs_${v}_$i.json 2>/dev/null
+      --steps 20 --warmup 5 --details gpurun_out/abs_${v}_$i.json > /dev/null 2>&1
     echo "== $v round $i"
     python3 tools/bench_summary.py gpurun_out/abs_${v}_$i.json
   done

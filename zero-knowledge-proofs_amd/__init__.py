@@ -1021,10 +1021,12 @@ class TorchExchange:
 
     def __init__(self, group=None):
         import torch.distributed as dist
-        self.dist, self.group = dist, group
+        self.dist, self.group, self.dead = dist, group, False
 
     def all_to_all(self, send_ptr, recv_ptr, chunk_bytes):
         import torch
+        if self.dead:
+            raise ExchangeError("TorchExchange: aborted")
         nbytes = chunk_bytes * self.dist.get_world_size(self.group)
         send = torch.frombuffer((C.c_uint8 * nbytes).from_address(send_ptr), dtype=torch.uint8)
         recv = torch.frombuffer((C.c_uint8 * nbytes).from_address(recv_ptr), dtype=torch.uint8)
@@ -1032,6 +1034,8 @@ class TorchExchange:
 
     def all_reduce_max(self, value):
         import torch
+        if self.dead:
+            raise ExchangeError("TorchExchange: aborted")
         t = torch.tensor([value], dtype=torch.int64)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
         return int(t.item())
@@ -1039,6 +1043,7 @@ class TorchExchange:
     def abort(self):
         if self.dist.is_initialized():
             self.dist.destroy_process_group(self.group)
+        self.group, self.dead = None, True   # the last reference: the group's connections close with it
 
 
 # ------------------------------------------------------------- verify ----

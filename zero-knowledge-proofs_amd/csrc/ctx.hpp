@@ -82,7 +82,12 @@ struct zk_pk_dev {
   uint32_t extras[zk::NUM_MSM] = {}; // extra bases appended (shard 0 only)
   // Window-shifted base copies (msm_precompute_windows): bases[slot] holds
   // win x (count + extras) points, window w = 2^(win_c w) x the base.
+  // The IC and H vectors are ONE MSM of the prove (both terms of pi_C):
+  // bases[MSM_H] holds win x (count[IC] + count[H]) points, each window the
+  // IC bases then the H bases (ich_tot() per window), and bases[MSM_IC] is
+  // empty once the windows are built.
   int win = 1, win_c = 0;
+  uint32_t ich_tot() const { return count[zk::MSM_IC] + extras[zk::MSM_IC] + count[zk::MSM_H] + extras[zk::MSM_H]; }
   // Bytes between consecutive bases of bases[slot]: 0 = packed (sizeof the
   // affine point), else padded to whole 128-B lines (msm_pad_bases).
   uint32_t stride[zk::NUM_MSM] = {};

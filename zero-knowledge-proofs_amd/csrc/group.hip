@@ -1,283 +1,461 @@
-// group.hip -- bucket grouping of the prove path's MSM entries without a
-// general radix sort (msm.hpp step 2, shared / batch plans with <= 16-bit
-// bucket ids and <= 4 windows: every prove MSM at c = 16).
+// group.hip -- bucket grouping of MSM entries (msm.hpp step 2): a stable LSD
+// counting sort written for gfx950 (round 6; replaced a separate digit-key
+// kernel + rocPRIM's onesweep radix sort + its passes).
 //
-// The accumulate needs the (point, window) entries grouped by bucket and
-// the first entry of every bucket (off[]); the order inside a bucket does
-// not matter (its entries are summed, and the group element is unique), so
-// this is a two-level counting sort keyed on the 16-bit bucket id (+ the
-// batch segment):
-//   count    per tile of 2048 points: the digits computed from the scalars,
-//            an LDS histogram of the coarse bin (bucket >> FINE_BITS), one
-//            column per tile (segment-major, then coarse bin, then tile);
-//   scan     one exclusive scan of those columns (rocPRIM): the first global
-//            position of every (coarse bin, tile);
-//   scatter  the same tiles again: entries ranked by coarse bin in LDS,
-//            staged there, then written out as contiguous runs per bin;
-//   fine     one workgroup per coarse bin (~8 K entries at 2^20): an LDS
-//            histogram of the fine bits, the bucket offsets written
-//            directly, then each entry moved to its bucket's range inside
-//            the bin (a 64-KB window of L2).
-// The keys are never materialised before grouping and nothing re-reads them
-// globally: against rocPRIM's onesweep (keys pass + histogram + two 9-bit
-// passes + offsets pass), ~32 instead of ~50 bytes per entry.
-#include <rocprim/device/device_scan.hpp>
-
+// An entry is one (point, digit window) pair: its key is the bucket (shared
+// plans: segment base + |digit| - 1, a zero digit the segment's bucket 0
+// with the dummy entry; per-window plans: window base + |digit| - 1, a zero
+// digit key G, which sorts after every bucket), its value the base index
+// with the digit's sign in bit 31.  The accumulate needs the entries grouped
+// by key and off[] (the first entry of every bucket).  The key bits split
+// into P digits of rb <= 8 bits (16-bit keys 2 x 8, the A+B1 batch's 17 bits
+// 3 x 6), least significant first; each pass is
+//   count    one workgroup per tile of GS_TE entries: an LDS histogram of the
+//            pass digit, written as column `tile` of a bin-major count matrix;
+//   scan     exclusive scan of the matrix (two kernels: chunk sums, then
+//            each chunk's prefix + its own scan): the output position of the
+//            first entry of every (bin, tile);
+//   scatter  the same tile again: every wave ranks its own contiguous part of
+//            the tile by digit (per-wave LDS counts, prefixed over the waves;
+//            inside a round of 64 entries the lane's rank among the lanes
+//            with its digit comes from ballots over the digit bits), stages
+//            the tile in LDS in output order and writes it out as one
+//            contiguous run per bin.
+// Ranks follow input order, so every pass is stable and the result is the
+// same bytes on every run (the XYZZ bucket sums, and the partials that
+// zk_groth16_prove_partial returns, are reproducible; no atomics decide an
+// order).  Pass 0 computes its entries from the scalars (in the count and
+// the scatter kernel: 8 B read per point, nothing materialised before the
+// first scatter); later passes read the previous pass's output.  Every pass
+// is load-balanced by construction (fixed-size tiles), whatever the digit
+// distribution (a witness of mostly 0 / 1 puts most entries in a few
+// buckets).  off[] then comes from the sorted keys (k_msm_offsets).
+// Digits of <= 8 bits (not the 9-10 of onesweep) keep a tile's run per bin
+// at >= 32 entries (128 B) of each array: same box, serial 2^20 prove, the
+// three MSM sorts 0.62 ms against onesweep's 0.70 (2 x 9 / 2 x 8 bits) and
+// 0.79 with 9-10-bit digits here (profiles/r06_ab_grouping.txt).
 #include "msm.hpp"
 
 namespace zk {
 
-constexpr uint32_t GRP_TP = 2048;              // points per tile
-constexpr uint32_t GRP_THREADS = 256;
-constexpr uint32_t GRP_FB = 7;                 // fine bits
-constexpr uint32_t GRP_NF = 1u << GRP_FB;      // fine bins per coarse bin
-constexpr uint32_t GRP_KB = 16;                // bucket bits of the plans this path takes
-constexpr uint32_t GRP_NC = 1u << (GRP_KB - GRP_FB);   // coarse bins per segment (512)
-constexpr uint32_t GRP_U = 8;                  // entries per thread per batch (fine pass)
+// tile shape (A/B builds: -DZK_GS_THREADS, -DZK_GS_IPT)
+#ifndef ZK_GS_THREADS
+#define ZK_GS_THREADS 512
+#endif
+#ifndef ZK_GS_IPT
+#define ZK_GS_IPT 16
+#endif
+constexpr uint32_t GS_THREADS = ZK_GS_THREADS;
+constexpr uint32_t GS_WAVES = GS_THREADS / 64;
+constexpr uint32_t GS_IPT = ZK_GS_IPT;              // entries per lane per tile
+constexpr uint32_t GS_TE = GS_THREADS * GS_IPT;     // entries per tile (8192)
+constexpr uint32_t GS_WR = GS_IPT;                  // rounds of 64 entries per wave
+// most digit bits per pass (A/B builds: -DZK_GS_RB)
+#ifndef ZK_GS_RB
+#define ZK_GS_RB 8
+#endif
+constexpr uint32_t GS_MAXRB = ZK_GS_RB;
+constexpr uint32_t GS_MAXNB = 1u << GS_MAXRB;
+constexpr int GS_MAXPASS = 3;
+constexpr uint32_t GS_SCAN_ITEMS = 8;               // scan: counters per thread
+constexpr uint32_t GS_SCAN_THREADS = 1024;
+constexpr uint32_t GS_SCAN_CHUNK = GS_SCAN_ITEMS * GS_SCAN_THREADS;
 
-struct GrpArgs {
+struct GsArgs {
   const uint64_t* sc[MSM_MAXSEG];
-  uint32_t n[MSM_MAXSEG], wstride[MSM_MAXSEG], ioff[MSM_MAXSEG];
-  uint32_t blk0[MSM_MAXSEG + 1];    // first tile of segment k
-  uint32_t ebase[MSM_MAXSEG + 1];   // first entry of segment k
-  uint32_t nseg, nwin, c, bits, kb;
+  uint32_t n[MSM_MAXSEG], wstride[MSM_MAXSEG], ioff[MSM_MAXSEG], kbase[MSM_MAXSEG];
+  uint32_t tile0[MSM_MAXSEG + 1];   // first pass-0 tile of segment k
+  uint32_t boff[MSM_MAXWIN];
+  uint32_t nseg, nwin, c, bits, shared, G, M, rb;
 };
 
-ZK_DI uint32_t grp_seg(const GrpArgs& a, uint32_t blk) {
+// Digit of window w of a scalar, given the carry out of window w - 1 (signed
+// windows, the top one unsigned), one window at a time.
+template <int SW>
+ZK_DI uint32_t gs_digit(const GsArgs& a, uint32_t w, const uint64_t (&s)[SW], uint32_t& carry, bool& neg) {
+  const bool top = w == a.nwin - 1;
+  const int width = top ? (int)(a.bits - a.c * w) : (int)a.c;
+  const uint32_t v = scal_window<SW>(s, (int)(a.c * w), width) + carry;
+  if (!top && v > (1u << (a.c - 1))) {
+    carry = 1;
+    neg = true;
+    return (1u << a.c) - v;
+  }
+  carry = 0;
+  neg = false;
+  return v;
+}
+
+// The entry of (segment k, point i, window w) with digit magnitude mag.
+ZK_DI void gs_entry(const GsArgs& a, uint32_t k, uint32_t i, uint32_t w, uint32_t mag, bool neg, uint32_t& key,
+                    uint32_t& ent) {
+  if (a.shared) {
+    key = a.kbase[k] + (mag ? mag - 1 : 0u);
+    ent = mag ? ((w * a.wstride[k] + a.ioff[k] + i) | (neg ? 0x80000000u : 0u)) : MSM_DUMMY;
+  } else {
+    key = mag ? a.boff[w] + mag - 1 : a.G;
+    ent = i | (neg ? 0x80000000u : 0u);
+  }
+}
+
+ZK_DI uint32_t gs_seg(const GsArgs& a, uint32_t tile) {
   uint32_t k = 0;
 #pragma unroll
   for (uint32_t j = 1; j < MSM_MAXSEG; j++)
-    if (j < a.nseg && blk >= a.blk0[j]) k = j;
+    if (j < a.nseg && tile >= a.tile0[j]) k = j;
   return k;
 }
 
-// Entry (point i of segment k, window w): its local bucket id (0 for a zero
-// digit, whose entry is the dummy) and its entry word, as k_msm_keys makes them
-// for shared plans.
-template <class F>
-ZK_DI void grp_entries(const GrpArgs& a, uint32_t k, uint32_t i, uint64_t s, F&& f) {
-  uint32_t carry = 0;
-  const uint32_t half = 1u << (a.c - 1);
-  for (uint32_t w = 0; w < a.nwin; w++) {
-    const bool top = w == a.nwin - 1;
-    const uint32_t off = a.c * w, width = top ? a.bits - off : a.c;
-    const uint32_t v = (uint32_t)((s >> off) & ((1ull << width) - 1)) + carry;
-    uint32_t mag;
+// The GS_IPT entries of this lane in tile `tile`, in input order.  Pass 0
+// (SRC): the tile is GS_TE / 64 units of segment k's (point round, window)
+// sequence, point-major (unit u = point round u / nwin, window u mod nwin);
+// wave v takes units [v GS_WR, (v + 1) GS_WR) and lane l point 64 pr + l of
+// a unit.  Consecutive units of one point round are consecutive windows, so
+// the signed-digit carry runs along them (the first unit of a wave recomputes
+// the carry of the windows below it).  Later passes: entries
+// tile GS_TE + v GS_WR 64 + 64 r + l of the input arrays.
+template <int SW, bool SRC>
+ZK_DI void gs_load(const GsArgs& a, uint32_t tile, const uint32_t* __restrict__ kin, const uint32_t* __restrict__ ein,
+                   uint32_t (&key)[GS_IPT], uint32_t (&ent)[GS_IPT], uint32_t& valid) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  valid = 0;
+  if constexpr (SRC) {
+    const uint32_t k = gs_seg(a, tile);
+    const uint32_t u0 = (tile - a.tile0[k]) * (GS_TE / 64) + wave * GS_WR;
+    const uint32_t nk = a.n[k];
+    uint32_t pr = u0 / a.nwin, w = u0 - pr * a.nwin;
+    uint32_t i = pr * 64 + lane;
+    uint64_t s[SW];
+    uint32_t carry = 0;
     bool neg = false;
-    if (!top && v > half) {
-      mag = (1u << a.c) - v;
-      neg = true;
-      carry = 1;
-    } else {
-      mag = v;
-      carry = 0;
+#pragma unroll
+    for (int j = 0; j < SW; j++) s[j] = i < nk ? a.sc[k][(size_t)i * SW + j] : 0ull;
+    for (uint32_t q = 0; q < w; q++) (void)gs_digit<SW>(a, q, s, carry, neg);
+#pragma unroll
+    for (uint32_t r = 0; r < GS_IPT; r++) {
+      key[r] = ent[r] = 0;
+      if (i < nk) {
+        const uint32_t mag = gs_digit<SW>(a, w, s, carry, neg);
+        gs_entry(a, k, i, w, mag, neg, key[r], ent[r]);
+        valid |= 1u << r;
+      }
+      if (++w == a.nwin) {   // next point round
+        w = 0;
+        carry = 0;
+        i += 64;
+#pragma unroll
+        for (int j = 0; j < SW; j++) s[j] = (r + 1 < GS_IPT && i < nk) ? a.sc[k][(size_t)i * SW + j] : 0ull;
+      }
     }
-    const uint32_t b = w * a.wstride[k] + a.ioff[k] + i;
-    f(mag ? mag - 1 : 0u, mag ? (b | (neg ? 0x80000000u : 0u)) : MSM_DUMMY, w);
-  }
-}
-// The tile's points i0 + threadIdx.x + GRP_THREADS j (GRP_TP / GRP_THREADS of
-// them per thread): every scalar load is issued before the first digit is
-// used, so the loads overlap instead of each waiting out its own latency.
-constexpr uint32_t GRP_PPT = GRP_TP / GRP_THREADS;
-template <class F>
-ZK_DI void grp_tile(const GrpArgs& a, uint32_t k, uint32_t i0, uint32_t i1, F&& f) {
-  uint64_t s[GRP_PPT];
-#pragma unroll
-  for (uint32_t j = 0; j < GRP_PPT; j++) {
-    const uint32_t i = i0 + threadIdx.x + GRP_THREADS * j;
-    s[j] = i < i1 ? a.sc[k][i] : 0ull;
-  }
-#pragma unroll
-  for (uint32_t j = 0; j < GRP_PPT; j++) {
-    const uint32_t i = i0 + threadIdx.x + GRP_THREADS * j;
-    if (i < i1) grp_entries(a, k, i, s[j], f);
-  }
-}
-
-__global__ void __launch_bounds__(GRP_THREADS) k_grp_count(GrpArgs a, uint32_t* __restrict__ cnt) {
-  __shared__ uint32_t hist[GRP_NC];
-  const uint32_t blk = blockIdx.x, k = grp_seg(a, blk), lb = blk - a.blk0[k];
-  const uint32_t nb = a.blk0[k + 1] - a.blk0[k];
-  for (uint32_t t = threadIdx.x; t < GRP_NC; t += GRP_THREADS) hist[t] = 0;
-  __syncthreads();
-  const uint32_t i0 = lb * GRP_TP, i1 = min(i0 + GRP_TP, a.n[k]);
-  grp_tile(a, k, i0, i1, [&](uint32_t key, uint32_t, uint32_t) { atomicAdd(&hist[key >> GRP_FB], 1u); });
-  __syncthreads();
-  const uint32_t base = GRP_NC * a.blk0[k];   // segment k's columns start here
-  for (uint32_t t = threadIdx.x; t < GRP_NC; t += GRP_THREADS) cnt[base + t * nb + lb] = hist[t];
-}
-
-// Exclusive scan of GRP_NC values in LDS (GRP_THREADS threads, 2 each).
-ZK_DI void grp_scan_nc(uint32_t* v, uint32_t* tmp) {
-  static_assert(GRP_NC == 2 * GRP_THREADS, "two bins per thread");
-  const uint32_t t = threadIdx.x;
-  const uint32_t a0 = v[2 * t], a1 = v[2 * t + 1];
-  tmp[t] = a0 + a1;
-  __syncthreads();
-  for (uint32_t d = 1; d < GRP_THREADS; d <<= 1) {   // inclusive Hillis-Steele over the pair sums
-    const uint32_t x = t >= d ? tmp[t - d] : 0u;
-    __syncthreads();
-    tmp[t] += x;
-    __syncthreads();
-  }
-  const uint32_t ex = tmp[t] - (a0 + a1);
-  v[2 * t] = ex;
-  v[2 * t + 1] = ex + a0;
-  __syncthreads();
-}
-
-__global__ void __launch_bounds__(GRP_THREADS) k_grp_scatter(GrpArgs a, const uint32_t* __restrict__ cnt,
-                                                             const uint32_t* __restrict__ cnt_off,
-                                                             uint32_t* __restrict__ tkey, uint32_t* __restrict__ tent) {
-  __shared__ uint32_t lbase[GRP_NC], lcur[GRP_NC], gbase[GRP_NC], stmp[GRP_THREADS];
-  __shared__ uint32_t skey[GRP_TP * 4], sent[GRP_TP * 4];   // nwin <= 4: 64 KB staging
-  const uint32_t blk = blockIdx.x, k = grp_seg(a, blk), lb = blk - a.blk0[k];
-  const uint32_t nb = a.blk0[k + 1] - a.blk0[k];
-  const uint32_t base = GRP_NC * a.blk0[k];
-  for (uint32_t t = threadIdx.x; t < GRP_NC; t += GRP_THREADS) lbase[t] = cnt[base + t * nb + lb];
-  __syncthreads();
-  grp_scan_nc(lbase, stmp);
-  for (uint32_t t = threadIdx.x; t < GRP_NC; t += GRP_THREADS) {
-    lcur[t] = lbase[t];
-    gbase[t] = cnt_off[base + t * nb + lb] - lbase[t];   // global position of local slot 0 of bin t
-  }
-  __syncthreads();
-  // rank by coarse bin (LDS atomics: order inside a bin is arbitrary) and stage
-  const uint32_t i0 = lb * GRP_TP, i1 = min(i0 + GRP_TP, a.n[k]);
-  const uint32_t kbase = k << a.kb;
-  grp_tile(a, k, i0, i1, [&](uint32_t key, uint32_t e, uint32_t) {
-    const uint32_t s = atomicAdd(&lcur[key >> GRP_FB], 1u);
-    skey[s] = kbase | key;
-    sent[s] = e;
-  });
-  __syncthreads();
-  // contiguous runs per bin: local slot j of bin t lands at gbase[t] + j
-  const uint32_t ne = (i1 > i0 ? i1 - i0 : 0) * a.nwin;
-  const uint32_t kmask = (1u << a.kb) - 1;
-  for (uint32_t j = threadIdx.x; j < ne; j += GRP_THREADS) {
-    const uint32_t key = skey[j];
-    const uint32_t g = gbase[(key & kmask) >> GRP_FB] + j;
-    tkey[g] = key;
-    tent[g] = sent[j];
-  }
-}
-
-__global__ void __launch_bounds__(GRP_THREADS) k_grp_fine(GrpArgs a, const uint32_t* __restrict__ cnt_off,
-                                                          const uint32_t* __restrict__ tkey,
-                                                          const uint32_t* __restrict__ tent, uint32_t* __restrict__ key,
-                                                          uint32_t* __restrict__ ent, uint32_t* __restrict__ off,
-                                                          uint32_t G) {
-  __shared__ uint32_t fcur[GRP_NF];
-  const uint32_t h = blockIdx.x, k = h / GRP_NC, cb = h % GRP_NC;
-  const uint32_t nb = a.blk0[k + 1] - a.blk0[k];
-  const uint32_t base = GRP_NC * a.blk0[k];
-  uint32_t S, E;
-  if (nb == 0) {
-    S = E = a.ebase[k];
   } else {
-    S = cnt_off[base + cb * nb];
-    E = cb + 1 < GRP_NC ? cnt_off[base + (cb + 1) * nb] : a.ebase[k + 1];
-  }
-  for (uint32_t t = threadIdx.x; t < GRP_NF; t += GRP_THREADS) fcur[t] = 0;
-  __syncthreads();
-  // batches of GRP_U entries per thread: their loads in flight together
-  constexpr uint32_t U = GRP_U;
-  for (uint32_t e0 = S; e0 < E; e0 += U * GRP_THREADS) {
-    uint32_t kk[U];
+    const size_t e0 = (size_t)tile * GS_TE + wave * GS_WR * 64 + lane;
 #pragma unroll
-    for (uint32_t u = 0; u < U; u++) {
-      const uint32_t e = e0 + threadIdx.x + GRP_THREADS * u;
-      kk[u] = e < E ? tkey[e] : 0xffffffffu;
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < U; u++)
-      if (kk[u] != 0xffffffffu) atomicAdd(&fcur[kk[u] & (GRP_NF - 1)], 1u);
-  }
-  __syncthreads();
-  if (threadIdx.x < 64) {   // exclusive scan of the 128 fine counts: one wave, 2 each
-    const uint32_t t = threadIdx.x, c0 = fcur[2 * t], c1 = fcur[2 * t + 1];
-    uint32_t incl = c0 + c1;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t x = __shfl_up(incl, d);
-      if (t >= (uint32_t)d) incl += x;
-    }
-    const uint32_t ex = S + incl - (c0 + c1);
-    fcur[2 * t] = ex;
-    fcur[2 * t + 1] = ex + c0;
-    const uint32_t g0 = (k << a.kb) | (cb << GRP_FB) | (2 * t);
-    off[g0] = ex;
-    off[g0 + 1] = ex + c0;
-  }
-  if (h == 0 && threadIdx.x == 0) off[G] = a.ebase[a.nseg];
-  __syncthreads();
-  for (uint32_t e0 = S; e0 < E; e0 += U * GRP_THREADS) {
-    uint32_t kk[U], ee[U];
-#pragma unroll
-    for (uint32_t u = 0; u < U; u++) {
-      const uint32_t e = e0 + threadIdx.x + GRP_THREADS * u;
-      kk[u] = e < E ? tkey[e] : 0xffffffffu;
-      ee[u] = e < E ? tent[e] : 0u;
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < U; u++) {
-      if (kk[u] == 0xffffffffu) continue;
-      const uint32_t pos = atomicAdd(&fcur[kk[u] & (GRP_NF - 1)], 1u);
-      key[pos] = kk[u];
-      ent[pos] = ee[u];
+    for (uint32_t r = 0; r < GS_IPT; r++) {
+      const size_t e = e0 + 64 * r;
+      const bool ok = e < a.M;
+      key[r] = ok ? kin[e] : 0u;
+      ent[r] = ok ? ein[e] : 0u;
+      if (ok) valid |= 1u << r;
     }
   }
 }
 
-bool msm_group_ok(const MsmPlan& p, int sw) {
-  return p.shared && sw == 1 && p.nwin <= 4 && (uint32_t)(p.kr[0] + p.kc[0]) == GRP_KB && p.nseg >= 1 &&
-         p.nseg <= MSM_MAXSEG;
+// count: column `tile` of the bin-major matrix cnt[b ntiles + tile]
+template <int SW, bool SRC>
+__global__ void __launch_bounds__(GS_THREADS) k_gs_count(GsArgs a, uint32_t shift, uint32_t ntiles,
+                                                         const uint32_t* __restrict__ kin,
+                                                         uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t h[GS_MAXNB];
+  const uint32_t NB = 1u << a.rb, tile = blockIdx.x;
+  for (uint32_t b = threadIdx.x; b < NB; b += GS_THREADS) h[b] = 0;
+  __syncthreads();
+  uint32_t key[GS_IPT], ent[GS_IPT], valid;
+  if constexpr (SRC) {
+    gs_load<SW, true>(a, tile, nullptr, nullptr, key, ent, valid);
+  } else {   // keys only
+    const size_t e0 = (size_t)tile * GS_TE + (threadIdx.x >> 6) * GS_WR * 64 + (threadIdx.x & 63);
+    valid = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < GS_IPT; r++) {
+      const size_t e = e0 + 64 * r;
+      key[r] = e < a.M ? kin[e] : 0u;
+      if (e < a.M) valid |= 1u << r;
+    }
+  }
+  (void)ent;
+#pragma unroll
+  for (uint32_t r = 0; r < GS_IPT; r++)
+    if (valid >> r & 1u) atomicAdd(&h[(key[r] >> shift) & (NB - 1)], 1u);
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < NB; b += GS_THREADS) cnt[(size_t)b * ntiles + tile] = h[b];
 }
 
-void msm_group(MsmWork& w, const MsmSeg* segs, int nseg, hipStream_t st) {
+// scan, kernel 1: the sum of every GS_SCAN_CHUNK counters
+__global__ void __launch_bounds__(GS_SCAN_THREADS) k_gs_scan_sums(const uint32_t* __restrict__ cnt, size_t L,
+                                                                  uint32_t* __restrict__ sums) {
+  __shared__ uint32_t ws[GS_SCAN_THREADS / 64];
+  const size_t base = (size_t)blockIdx.x * GS_SCAN_CHUNK;
+  uint32_t s = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < GS_SCAN_ITEMS; j++) {
+    const size_t i = base + j * GS_SCAN_THREADS + threadIdx.x;
+    if (i < L) s += cnt[i];
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (uint32_t v = 0; v < GS_SCAN_THREADS / 64; v++) t += ws[v];
+    sums[blockIdx.x] = t;
+  }
+}
+
+// Exclusive scan of one value per thread over the workgroup (wave shuffles,
+// then the wave totals); returns the thread's exclusive prefix, total in *tot.
+template <uint32_t THREADS>
+ZK_DI uint32_t gs_block_scan(uint32_t v, uint32_t* ws, uint32_t* tot) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t x = __shfl_up(incl, d);
+    if (lane >= (uint32_t)d) incl += x;
+  }
+  if (lane == 63) ws[wave] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (uint32_t w = 0; w < THREADS / 64; w++) {
+      const uint32_t t = ws[w];
+      ws[w] = s;
+      s += t;
+    }
+    ws[THREADS / 64] = s;
+  }
+  __syncthreads();
+  const uint32_t ex = ws[wave] + incl - v;
+  if (tot) *tot = ws[THREADS / 64];
+  __syncthreads();   // ws reusable
+  return ex;
+}
+
+// scan, kernel 2: chunk b's offset (the sums of the chunks before it) plus
+// the exclusive scan of its own counters, in place
+__global__ void __launch_bounds__(GS_SCAN_THREADS) k_gs_scan_apply(uint32_t* __restrict__ cnt, size_t L,
+                                                                   const uint32_t* __restrict__ sums) {
+  __shared__ uint32_t ws[GS_SCAN_THREADS / 64 + 1];
+  __shared__ uint32_t red[GS_SCAN_THREADS / 64];
+  // offset of this chunk
+  uint32_t o = 0;
+  for (uint32_t j = threadIdx.x; j < blockIdx.x; j += GS_SCAN_THREADS) o += sums[j];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) o += __shfl_xor(o, d);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = o;
+  __syncthreads();
+  uint32_t off = 0;
+  for (uint32_t v = 0; v < GS_SCAN_THREADS / 64; v++) off += red[v];
+  // thread t scans counters [t ITEMS, (t + 1) ITEMS) of the chunk (contiguous)
+  const size_t base = (size_t)blockIdx.x * GS_SCAN_CHUNK + (size_t)threadIdx.x * GS_SCAN_ITEMS;
+  uint32_t c[GS_SCAN_ITEMS], s = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < GS_SCAN_ITEMS; j++) {
+    c[j] = base + j < L ? cnt[base + j] : 0u;
+    s += c[j];
+  }
+  uint32_t ex = gs_block_scan<GS_SCAN_THREADS>(s, ws, nullptr) + off;
+#pragma unroll
+  for (uint32_t j = 0; j < GS_SCAN_ITEMS; j++) {
+    if (base + j < L) cnt[base + j] = ex;
+    ex += c[j];
+  }
+}
+
+// scatter: rank, stage, write out (see the file comment)
+template <int SW, bool SRC>
+__global__ void __launch_bounds__(GS_THREADS) k_gs_scatter(GsArgs a, uint32_t shift, uint32_t ntiles,
+                                                           const uint32_t* __restrict__ kin,
+                                                           const uint32_t* __restrict__ ein,
+                                                           const uint32_t* __restrict__ pos,
+                                                           uint32_t* __restrict__ kout, uint32_t* __restrict__ eout) {
+  __shared__ uint32_t sk[GS_TE], se[GS_TE];
+  __shared__ uint32_t wh[GS_WAVES][GS_MAXNB];   // per-wave counts -> per-wave running slot
+  __shared__ uint32_t tb[GS_MAXNB];             // output position of local slot 0 of bin b
+  __shared__ uint32_t ws[GS_THREADS / 64 + 1];
+  const uint32_t NB = 1u << a.rb, tile = blockIdx.x;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (uint32_t j = threadIdx.x; j < GS_WAVES * GS_MAXNB; j += GS_THREADS) (&wh[0][0])[j] = 0;
+  uint32_t key[GS_IPT], ent[GS_IPT], valid;
+  gs_load<SW, SRC>(a, tile, kin, ein, key, ent, valid);
+  __syncthreads();
+#pragma unroll
+  for (uint32_t r = 0; r < GS_IPT; r++)
+    if (valid >> r & 1u) atomicAdd(&wh[wave][(key[r] >> shift) & (NB - 1)], 1u);
+  __syncthreads();
+  // per bin: the waves' exclusive prefix (in wh) and the tile count, then
+  // the local slot of the bin's first entry (scan over bins, GS_BPT
+  // consecutive bins per thread)
+  constexpr uint32_t GS_BPT = GS_MAXNB > GS_THREADS ? GS_MAXNB / GS_THREADS : 1;
+  uint32_t tc[GS_BPT], tsum = 0;
+#pragma unroll
+  for (uint32_t h = 0; h < GS_BPT; h++) {
+    const uint32_t b = GS_BPT * threadIdx.x + h;
+    tc[h] = 0;
+    if (b < NB) {
+      uint32_t s = 0;
+      for (uint32_t v = 0; v < GS_WAVES; v++) {
+        const uint32_t c = wh[v][b];
+        wh[v][b] = s;
+        s += c;
+      }
+      tc[h] = s;
+    }
+    tsum += tc[h];
+  }
+  uint32_t lb = gs_block_scan<GS_THREADS>(tsum, ws, nullptr);
+#pragma unroll
+  for (uint32_t h = 0; h < GS_BPT; h++) {
+    const uint32_t b = GS_BPT * threadIdx.x + h;
+    if (b < NB) {
+      tb[b] = pos[(size_t)b * ntiles + tile] - lb;
+      for (uint32_t v = 0; v < GS_WAVES; v++) wh[v][b] += lb;
+    }
+    lb += tc[h];
+  }
+  __syncthreads();
+  // rank in input order: rounds in order, lanes in order inside a round
+  const uint64_t lt_mask = (1ull << lane) - 1;
+  uint32_t cnt = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < GS_IPT; r++) {
+    const bool ok = valid >> r & 1u;
+    const uint32_t d = (key[r] >> shift) & (NB - 1);
+    uint64_t m = __ballot(ok);
+    for (uint32_t bit = 0; bit < a.rb; bit++) {
+      const uint64_t bb = __ballot((d >> bit) & 1u);
+      m &= ((d >> bit) & 1u) ? bb : ~bb;
+    }
+    if (ok) {
+      const uint32_t base = wh[wave][d];
+      const uint32_t slot = base + __popcll(m & lt_mask);
+      sk[slot] = key[r];
+      se[slot] = ent[r];
+      if ((m & lt_mask) == 0) wh[wave][d] = base + __popcll(m);   // the lowest lane of the digit
+      cnt++;
+    }
+  }
+  // tile total
+  uint32_t tot = 0;
+  (void)gs_block_scan<GS_THREADS>(cnt, ws, &tot);
+  // contiguous runs per bin: local slot j of bin b lands at tb[b] + j
+  for (uint32_t j = threadIdx.x; j < tot; j += GS_THREADS) {
+    const uint32_t k = sk[j];
+    const uint32_t g = tb[(k >> shift) & (NB - 1)] + j;
+    kout[g] = k;
+    eout[g] = se[j];
+  }
+}
+
+// off[g] = first sorted position with key >= g, for g in [0, G].
+// ctl (MsmWork::nbig): the merge's and the fixup list's control words,
+// zeroed here so that no memset launch is needed.
+__global__ void __launch_bounds__(256) k_msm_offsets(const uint32_t* __restrict__ key, uint32_t M, uint32_t G,
+                                                     uint32_t* __restrict__ off, uint32_t* __restrict__ ctl) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 3) ctl[i] = 0;
+  if (i > M) return;
+  const uint32_t lo = i ? min(key[i - 1], G) + 1 : 0;     // keys in (key[i-1], key[i]] start at i
+  const uint32_t hi = i < M ? min(key[i], G) : G;
+  for (uint32_t g = lo; g <= hi; g++) off[g] = i;
+}
+
+void msm_offsets(MsmWork& w, uint32_t M, hipStream_t st) {
+  w.nbig.ensure(3 * sizeof(uint32_t));
+  k_msm_offsets<<<ceil_div((uint64_t)M + 1, 256), 256, 0, st>>>(w.key.as<uint32_t>(), M, w.plan.G,
+                                                                 w.off.as<uint32_t>(), w.nbig.as<uint32_t>());
+  ZK_LAUNCH_CHECK();
+}
+
+template <int SW>
+static void gs_run(MsmWork& w, const GsArgs& a, uint32_t ntiles0, hipStream_t st) {
   const MsmPlan& p = w.plan;
-  GrpArgs a{};
+  const uint32_t M = a.M;
+  uint32_t maxkey = p.shared ? p.G - 1 : p.G;
+  uint32_t kb = 1;
+  while (kb < 32 && (maxkey >> kb)) kb++;
+  const uint32_t P = (kb + GS_MAXRB - 1) / GS_MAXRB;
+  GsArgs g = a;
+  g.rb = (kb + P - 1) / P;
+  const uint32_t NB = 1u << g.rb;
+  const uint32_t ntiles1 = ceil_div(M, GS_TE);
+  const size_t L = (size_t)NB * std::max(ntiles0, ntiles1);
+  w.gcnt.ensure(sizeof(uint32_t) * std::max<size_t>(L, 1));
+  w.gcnt_sums.ensure(sizeof(uint32_t) * (L / GS_SCAN_CHUNK + 2));
+  uint32_t* cnt = w.gcnt.as<uint32_t>();
+  uint32_t* sums = w.gcnt_sums.as<uint32_t>();
+  // ping-pong so that the last pass writes w.key / w.ent
+  uint32_t* kbuf[2] = {w.key.as<uint32_t>(), w.key_in.as<uint32_t>()};
+  uint32_t* ebuf[2] = {w.ent.as<uint32_t>(), w.ent_in.as<uint32_t>()};
+  const uint32_t* kin = nullptr;
+  const uint32_t* ein = nullptr;
+  for (uint32_t pass = 0; pass < P; pass++) {
+    const uint32_t shift = pass * g.rb;
+    const uint32_t nt = pass == 0 ? ntiles0 : ntiles1;
+    const size_t Lp = (size_t)NB * nt;
+    if (pass == 0)
+      k_gs_count<SW, true><<<nt, GS_THREADS, 0, st>>>(g, shift, nt, nullptr, cnt);
+    else
+      k_gs_count<SW, false><<<nt, GS_THREADS, 0, st>>>(g, shift, nt, kin, cnt);
+    ZK_LAUNCH_CHECK();
+    const uint32_t nchunk = ceil_div(Lp, GS_SCAN_CHUNK);
+    k_gs_scan_sums<<<nchunk, GS_SCAN_THREADS, 0, st>>>(cnt, Lp, sums);
+    ZK_LAUNCH_CHECK();
+    k_gs_scan_apply<<<nchunk, GS_SCAN_THREADS, 0, st>>>(cnt, Lp, sums);
+    ZK_LAUNCH_CHECK();
+    const uint32_t out = (P - 1 - pass) & 1u;
+    if (pass == 0)
+      k_gs_scatter<SW, true><<<nt, GS_THREADS, 0, st>>>(g, shift, nt, nullptr, nullptr, cnt, kbuf[out], ebuf[out]);
+    else
+      k_gs_scatter<SW, false><<<nt, GS_THREADS, 0, st>>>(g, shift, nt, kin, ein, cnt, kbuf[out], ebuf[out]);
+    ZK_LAUNCH_CHECK();
+    kin = kbuf[out];
+    ein = ebuf[out];
+  }
+}
+
+void msm_group(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hipStream_t st) {
+  const MsmPlan& p = w.plan;
+  GsArgs a{};
   a.nseg = (uint32_t)nseg;
   a.nwin = (uint32_t)p.nwin;
   a.c = (uint32_t)p.c;
   a.bits = (uint32_t)p.bits;
-  a.kb = GRP_KB;
-  uint32_t blk = 0, e = 0;
+  a.shared = p.shared ? 1u : 0u;
+  a.G = p.G;
+  for (int k = 0; k < p.nwin && k < MSM_MAXWIN; k++) a.boff[k] = p.boff[k];
+  uint32_t tiles = 0;
+  size_t M = 0;
   for (int k = 0; k < nseg; k++) {
     a.sc[k] = segs[k].scalars;
     a.n[k] = segs[k].n;
     a.wstride[k] = segs[k].wstride ? segs[k].wstride : segs[k].n;
     a.ioff[k] = segs[k].ioff;
-    a.blk0[k] = blk;
-    a.ebase[k] = e;
-    blk += ceil_div(segs[k].n, GRP_TP);
-    e += segs[k].n * (uint32_t)p.nwin;
+    a.kbase[k] = (p.shared && nseg > 1) ? (uint32_t)k << (p.segshift & 31) : 0u;
+    a.tile0[k] = tiles;
+    const uint64_t rounds = (uint64_t)ceil_div(segs[k].n, 64) * (uint64_t)p.nwin;
+    tiles += (uint32_t)((rounds + GS_TE / 64 - 1) / (GS_TE / 64));
+    M += (size_t)segs[k].n * p.nwin;
   }
-  for (int k = nseg; k <= MSM_MAXSEG; k++) {
-    a.blk0[k] = blk;
-    a.ebase[k] = e;
+  for (int k = nseg; k <= MSM_MAXSEG; k++) a.tile0[k] = tiles;
+  a.M = (uint32_t)M;
+  if (M) {
+    w.key_in.ensure(sizeof(uint32_t) * M);
+    w.ent_in.ensure(sizeof(uint32_t) * M);
+    if (sw == 1) gs_run<1>(w, a, tiles, st);
+    else gs_run<4>(w, a, tiles, st);
   }
-  const size_t ncnt = (size_t)GRP_NC * blk;
-  w.gcnt.ensure(sizeof(uint32_t) * std::max<size_t>(ncnt, 1));
-  w.gcnt_off.ensure(sizeof(uint32_t) * std::max<size_t>(ncnt, 1));
-  if (blk) {
-    k_grp_count<<<blk, GRP_THREADS, 0, st>>>(a, w.gcnt.as<uint32_t>());
-    ZK_LAUNCH_CHECK();
-    size_t tmp_bytes = 0;
-    ZK_HIP(rocprim::exclusive_scan(nullptr, tmp_bytes, w.gcnt.as<uint32_t>(), w.gcnt_off.as<uint32_t>(), 0u, ncnt,
-                                   rocprim::plus<uint32_t>(), st));
-    w.sort_tmp.ensure(std::max<size_t>(tmp_bytes, 1));
-    ZK_HIP(rocprim::exclusive_scan(w.sort_tmp.p, tmp_bytes, w.gcnt.as<uint32_t>(), w.gcnt_off.as<uint32_t>(), 0u,
-                                   ncnt, rocprim::plus<uint32_t>(), st));
-    k_grp_scatter<<<blk, GRP_THREADS, 0, st>>>(a, w.gcnt.as<uint32_t>(), w.gcnt_off.as<uint32_t>(),
-                                                w.key_in.as<uint32_t>(), w.ent_in.as<uint32_t>());
-    ZK_LAUNCH_CHECK();
-  }
-  k_grp_fine<<<(uint32_t)nseg * GRP_NC, GRP_THREADS, 0, st>>>(a, w.gcnt_off.as<uint32_t>(), w.key_in.as<uint32_t>(),
-                                                               w.ent_in.as<uint32_t>(), w.key.as<uint32_t>(),
-                                                               w.ent.as<uint32_t>(), w.off.as<uint32_t>(), p.G);
-  ZK_LAUNCH_CHECK();
+  msm_offsets(w, (uint32_t)M, st);
 }
 
 }  // namespace zk

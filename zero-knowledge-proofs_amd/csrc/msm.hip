@@ -110,83 +110,6 @@ static MsmPlan msm_make_plan_batch(const MsmSeg* segs, int nseg, int bits, int c
   return p;
 }
 
-// ------------------------------------------------------------- digits ---
-template <int SW>
-__device__ __forceinline__ uint32_t scal_window(const uint64_t (&s)[SW], int off, int width) {
-  int wd = off >> 6, sh = off & 63;
-  uint64_t lo = 0;
-#pragma unroll
-  for (int k = 0; k < SW; k++)
-    if (k == wd) lo = s[k] >> sh;
-  if (sh + width > 64) {
-#pragma unroll
-    for (int k = 0; k < SW; k++)
-      if (k == wd + 1) lo |= s[k] << (64 - sh);
-  }
-  return (uint32_t)(lo & ((1ull << width) - 1));
-}
-
-
-// Radix-sort path: one (bucket, entry) pair per (point, window), written
-// window-major (coalesced); a zero digit gets the key G, which sorts after
-// every bucket, so off[G] still counts the non-zero digits.
-// Batches call it once per MSM with that MSM's n, its first bucket key_base
-// and key / ent advanced to its first entry.
-// wstride / ioff (shared plans): the segment's point i is base ioff + i of
-// a window-shifted vector whose windows are wstride points apart.
-template <int SW>
-__global__ void __launch_bounds__(256) k_msm_keys(const uint64_t* __restrict__ sc, MsmPlan p, uint32_t n,
-                                                  uint32_t key_base, uint32_t wstride, uint32_t ioff,
-                                                  uint32_t* __restrict__ key, uint32_t* __restrict__ ent) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint64_t s[SW];
-#pragma unroll
-  for (int k = 0; k < SW; k++) s[k] = sc[(size_t)i * SW + k];
-  uint32_t carry = 0;
-  const uint32_t half = 1u << (p.c - 1);
-  for (int w = 0; w < p.nwin; w++) {
-    const bool top = (w == p.nwin - 1);
-    const int width = top ? p.bits - p.c * w : p.c;
-    const uint32_t v = scal_window<SW>(s, p.c * w, width) + carry;
-    uint32_t mag;
-    bool neg = false;
-    if (!top && v > half) {
-      mag = (1u << p.c) - v;
-      neg = true;
-      carry = 1;
-    } else {
-      mag = v;
-      carry = 0;
-    }
-    const size_t o = (size_t)w * n + i;
-    if (p.shared) {
-      // shared buckets: keys stay < 2^16 per MSM (two 8-bit radix passes
-      // for one) -- a zero digit becomes a dummy entry of the MSM's bucket 0
-      // that adds nothing
-      key[o] = key_base + (mag ? mag - 1 : 0u);
-      const uint32_t b = (uint32_t)w * wstride + ioff + i;   // base 2^(c w) P_i
-      ent[o] = mag ? (b | (neg ? 0x80000000u : 0u)) : MSM_DUMMY;
-    } else {
-      key[o] = mag ? p.boff[w] + mag - 1 : p.G;
-      ent[o] = i | (neg ? 0x80000000u : 0u);
-    }
-  }
-}
-
-// off[g] = first sorted position with key >= g, for g in [0, G].
-// ctl (MsmWork::nbig): the merge's control words, zeroed here so that the
-// back phase needs no memset launch of its own.
-__global__ void __launch_bounds__(256) k_msm_offsets(const uint32_t* __restrict__ key, uint32_t M, uint32_t G,
-                                                     uint32_t* __restrict__ off, uint32_t* __restrict__ ctl) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < 2) ctl[i] = 0;
-  if (i > M) return;
-  const uint32_t lo = i ? min(key[i - 1], G) + 1 : 0;     // keys in (key[i-1], key[i]] start at i
-  const uint32_t hi = i < M ? min(key[i], G) : G;
-  for (uint32_t g = lo; g <= hi; g++) off[g] = i;
-}
-
 // --------------------------------------------------------- accumulate ---
 
 // Chunk length: the M grouped entries (known on device only) split evenly
@@ -207,6 +130,15 @@ __device__ __forceinline__ uint32_t chunk_len(uint32_t M, uint32_t T) {
 // XCD (~6 MB) outgrow its 4 MB L2: each line came back from the fabric up to
 // 32 times; now at most 128 B / (4 B x ENTQ) = 2.  Reads may run ENTQ - 1
 // entries past the chunk (the arrays carry that slack).
+// G1: complete the buckets split over two chunks of one wave at the end of
+// the accumulate and list the rest for the fixup (k_msm_fixup_list);
+// ZK_FIX_INWAVE=0: A/B build with the per-bucket fixup of round 5
+#ifndef ZK_FIX_INWAVE
+#define ZK_FIX_INWAVE 1
+#endif
+#ifndef ZK_FIX_INWAVE_G2
+#define ZK_FIX_INWAVE_G2 1
+#endif
 constexpr uint32_t ENTQ = 16;
 constexpr uint32_t ENTQ_LDS_WORDS = 2 * ENTQ * 64;   // per wave
 struct EntQ {
@@ -280,7 +212,9 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_G1_ATTR k_msm_accum(SegBases<typ
                                                    const uint32_t* __restrict__ key,
                                                    const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
                                                    typename C::X* __restrict__ buckets,
-                                                   typename C::X* __restrict__ partials) {
+                                                   typename C::X* __restrict__ partials,
+                                                   uint32_t* __restrict__ ctl, uint32_t* __restrict__ fixlist,
+                                                   uint32_t inwave) {
   using X = typename C::X;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t M = off[G];  // grouped entries (known on device only)
@@ -315,6 +249,36 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_G1_ATTR k_msm_accum(SegBases<typ
   if (head) st_vec(&partials[2 * (size_t)t], acc);
   else if (tail) st_vec(&partials[2 * (size_t)t + 1], acc);
   else st_vec(&buckets[cur], acc);
+  if (ZK_FIX_INWAVE && inwave) {
+    // Buckets split over chunks t and t + 1 of the same wave (the common
+    // case for a batch: a bucket holds about one chunk's worth of entries)
+    // are completed here: the next lane's head piece is in memory (its own
+    // flush above), one add with that operand from memory.  Every other
+    // bucket that this chunk begins and a later one continues goes on the
+    // fixup list (ctl[2]), so the fixup touches only those.  Single G1 MSMs
+    // (H: buckets over ~4-6 chunks, so hardly any pair) keep the per-bucket
+    // fixup (inwave = 0): there the list only added a dependent load.
+    const uint32_t lane = threadIdx.x & 63;
+    const bool opens = tail && !head;   // this chunk holds the bucket's first entry
+    bool pair = opens && lane != 63 && off[cur + 1] <= end + K;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the wave's flushes, before the neighbours read them
+    bool listed = opens && !pair;
+    if (pair) {
+      bool dbl;
+      const Fq* q = reinterpret_cast<const Fq*>(&partials[2 * (size_t)t + 2]);
+      const X sum = xyzz_add_mem(acc, [&](int k) { return ld_vec(q + k); }, &dbl);
+      if (dbl) listed = true;   // p == q: the fixup's add doubles
+      else st_vec(&buckets[cur], sum);
+    }
+    const uint64_t lm = __ballot(listed);
+    if (lm) {
+      const uint32_t leader = (uint32_t)__ffsll((long long)lm) - 1;
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(&ctl[2], (uint32_t)__popcll(lm));
+      base = __shfl(base, (int)leader);
+      if (listed) fixlist[base + __popcll(lm & ((1ull << lane) - 1))] = cur;
+    }
+  }
 }
 
 // G2 accumulate over lane pairs (Fq2h, ff.hpp): chunk t is owned by lanes
@@ -333,7 +297,9 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_G2_ATTR k_msm_accum_pair(SegBase
                                                                       const uint32_t* __restrict__ key,
                                                                       const uint32_t* __restrict__ off, uint32_t G,
                                                                       uint32_t T, G2X* __restrict__ buckets,
-                                                                      G2X* __restrict__ partials) {
+                                                                      G2X* __restrict__ partials,
+                                                                      uint32_t* __restrict__ ctl,
+                                                                      uint32_t* __restrict__ fixlist) {
   const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
   const uint32_t h = pair_half();
   const uint32_t M = off[G];
@@ -368,6 +334,32 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_G2_ATTR k_msm_accum_pair(SegBase
   if (head) st_pair(&partials[2 * (size_t)t], acc);
   else if (tail) st_pair(&partials[2 * (size_t)t + 1], acc);
   else st_pair(&buckets[cur], acc);
+  if constexpr (ZK_FIX_INWAVE_G2) {
+    // as k_msm_accum: the buckets split over two chunks of one wave (32 lane
+    // pairs) are completed here, the others listed for the fixup (by the
+    // pair's even lane); every branch below is pair-uniform
+    const uint32_t pl = (threadIdx.x & 63) >> 1;
+    const bool opens = tail && !head;
+    bool pair = opens && pl != 31 && off[cur + 1] <= end + K;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    bool listed = opens && !pair;
+    if (pair) {
+      bool dbl;
+      const Fq* q = reinterpret_cast<const Fq*>(&partials[2 * (size_t)t + 2]) + h;
+      const XYZZ<Fq2h> sum = xyzz_add_mem(acc, [&](int k) { return Fq2h{ld_vec(q + 2 * k)}; }, &dbl);
+      if (dbl) listed = true;
+      else st_pair(&buckets[cur], sum);
+    }
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t lm = __ballot(listed && h == 0);
+    if (lm) {
+      const uint32_t leader = (uint32_t)__ffsll((long long)lm) - 1;
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(&ctl[2], (uint32_t)__popcll(lm));
+      base = __shfl(base, (int)leader);
+      if (listed && h == 0) fixlist[base + __popcll(lm & ((1ull << lane) - 1))] = cur;
+    }
+  }
 }
 
 // Buckets whose entries span several accumulate chunks.  A bucket over
@@ -454,6 +446,32 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
   if (t0 == t1) return;
   if (t1 - t0 + 1 > fix_max) {   // left to the merge levels, which skip themselves when none exist
     atomicAdd(nbig, 1u);
+    return;
+  }
+  X acc = ld_vec(&partials[2 * (size_t)t0 + 1]);
+  for (uint32_t t = t0 + 1; t <= t1; t++) acc = tail_add(acc, ld_vec(&partials[2 * (size_t)t]));
+  st_vec(&buckets[g], acc);
+}
+
+// The fixup of the listed buckets (ZK_FIX_INWAVE): ctl[2] buckets that the
+// accumulate could not complete in its own wave, each summed serially from
+// its chunk pieces by one thread (the list's order does not matter: each
+// thread writes its own bucket, in chunk order), buckets over more than
+// fix_max chunks left to the merge.
+template <class C>
+__global__ void __launch_bounds__(128) k_msm_fixup_list(const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
+                                                        uint32_t fix_max, uint32_t* __restrict__ ctl,
+                                                        const uint32_t* __restrict__ list,
+                                                        typename C::X* __restrict__ buckets,
+                                                        const typename C::X* __restrict__ partials) {
+  using X = typename C::X;
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= ctl[2]) return;
+  const uint32_t K = chunk_len(off[G], T);
+  const uint32_t g = list[u];
+  const uint32_t t0 = off[g] / K, t1 = (off[g + 1] - 1) / K;
+  if (t1 - t0 + 1 > fix_max) {   // left to the merge levels
+    atomicAdd(&ctl[0], 1u);
     return;
   }
   X acc = ld_vec(&partials[2 * (size_t)t0 + 1]);
@@ -923,6 +941,27 @@ __global__ void __launch_bounds__(128) k_msm_fixup_pair(const uint32_t* __restri
   st_pair(&buckets[g], acc);
 }
 
+// The G2 listed-bucket fixup (ZK_FIX_INWAVE_G2) on lane pairs.
+__global__ void __launch_bounds__(128) k_msm_fixup_list_pair(const uint32_t* __restrict__ off, uint32_t G,
+                                                             uint32_t T, uint32_t fix_max, uint32_t* __restrict__ ctl,
+                                                             const uint32_t* __restrict__ list,
+                                                             G2X* __restrict__ buckets,
+                                                             const G2X* __restrict__ partials) {
+  const uint32_t u = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;   // pair-uniform from here on
+  if (u >= ctl[2]) return;
+  const uint32_t K = chunk_len(off[G], T);
+  const uint32_t g = list[u];
+  const uint32_t t0 = off[g] / K, t1 = (off[g + 1] - 1) / K;
+  if (t1 - t0 + 1 > fix_max) {
+    if (!pair_half()) atomicAdd(&ctl[0], 1u);
+    return;
+  }
+  XYZZ<Fq2h> acc = ld_pair(&partials[2 * (size_t)t0 + 1]);
+#pragma unroll 1
+  for (uint32_t t = t0 + 1; t <= t1; t++) acc = tail_add(acc, ld_pair(&partials[2 * (size_t)t]));
+  st_pair(&buckets[g], acc);
+}
+
 // Two parts of one split MSM (msm_batch_back COMBINE): bucket g = this
 // part's bucket + the earlier part's, each only where its part had entries,
 // written for EVERY bucket (infinity where both are empty), so the reduction
@@ -959,8 +998,6 @@ __global__ void __launch_bounds__(128) k_msm_combine_pair(const uint32_t* __rest
 }
 
 // ------------------------------------------------------------ driver -----
-void sort_pairs_u32(void* tmp, size_t& tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
-                    const uint32_t* vals_in, uint32_t* vals_out, size_t n, unsigned end_bit, hipStream_t st);
 
 // Accumulate threads: one full-occupancy round of the chip (blocks per CU
 // from the occupancy calculator x CUs x 128; G2 runs two lanes per chunk).
@@ -1062,19 +1099,9 @@ static void msm_split_sums(MsmPlan& p, uint32_t target, uint32_t lanes) {
   }
 }
 
-// Bucket grouping of the prove path's plans by group.hip's counting passes
-// instead of k_msm_keys + rocPRIM onesweep + k_msm_offsets: 0 (default)
-// never, 1 every plan it takes, 2 single-MSM plans only (G2, H); A/B builds.
-// Round 5: serial sorts G2 0.136 -> 0.089 ms, H 0.117 -> 0.087 ms; with the
-// A+B1+IC batch as well (1) the overlapped prove lost 0.08-0.15 ms, with 2 it
-// is unchanged (9.067 vs 9.040 ms, median of 5, profiles/r05_ab_grouping.txt).
-// Not the default: the order inside a bucket then follows LDS atomics, so
-// the XYZZ bucket sums -- and the partials zk_groth16_prove_partial returns --
-// differ in their bytes from run to run (the same points; the proof bytes do
-// not change), and the sorted order keeps every partial reproducible.
-#ifndef ZK_MSM_GROUP
-#define ZK_MSM_GROUP 0
-#endif
+// G1 plans whose accumulate completes two-chunk buckets in its waves and
+// lists the rest (ZK_FIX_INWAVE): batches (the A+B1+IC MSMs)
+static inline uint32_t g1_inwave(const MsmPlan& p) { return ZK_FIX_INWAVE && p.nseg > 1 ? 1u : 0u; }
 
 // Buckets spread over at most this many accumulate chunks are summed by the
 // serial fixup; larger ones go through the log-depth merge.
@@ -1105,6 +1132,7 @@ static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hip
   // (profiles/r05_ab_qtail_slowbox.txt)
   if (g2 ? ZK_SPLIT_G2 : ZK_SPLIT_G1) msm_split_sums(p, rowcol_waves<C>(), g2 ? 32u : 64u);
   w.partials.ensure(sizeof(X) * 2 * (size_t)p.T);
+  w.fixlist.ensure(sizeof(uint32_t) * std::max<uint32_t>(std::min(p.G, p.T), 1));
   w.partials2.ensure(sizeof(X) * ((size_t)p.T / 2 + 2));
   w.rc.ensure(sizeof(X) * p.nrc);
   w.res.ensure(sizeof(X) * p.nq);
@@ -1118,46 +1146,9 @@ static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hip
 
   Prof* pf = w.prof;
   int ph = pf ? pf->begin(st, (w.tag + "msm_sort").c_str(), n) : -1;
-  w.key_in.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
-  w.ent_in.ensure(sizeof(uint32_t) * std::max<size_t>(M, 1));
-  w.nbig.ensure(2 * sizeof(uint32_t));
-  if (ZK_MSM_GROUP && msm_group_ok(p, sw) && (ZK_MSM_GROUP == 1 || nseg == 1)) {
-    // the prove path's plans: two-level counting grouping (group.hip)
-    msm_group(w, segs, nseg, st);
-    ZK_HIP(hipMemsetAsync(w.nbig.p, 0, 2 * sizeof(uint32_t), st));
-    if (pf) pf->end(st, ph);
-  } else {
-  // group the (point, window) entries by bucket: rocPRIM radix sort on
-  // ceil(log2(G + 1)) key bits (log2(G) when shared)
-  unsigned end_bit = 1;
-  while ((1ull << end_bit) < (uint64_t)p.G + (p.shared ? 0 : 1)) end_bit++;
-  size_t tmp_bytes = 0;
-  sort_pairs_u32(nullptr, tmp_bytes, nullptr, nullptr, nullptr, nullptr, M, end_bit, st);
-  w.sort_tmp.ensure(tmp_bytes);
-  size_t eoff = 0;
-  for (int k = 0; k < nseg; k++) {
-    const uint32_t nk = segs[k].n;
-    if (!nk) continue;
-    const uint32_t nb = ceil_div(nk, 256);
-    const uint32_t kbase = p.shared ? (uint32_t)k << (p.segshift & 31) : 0u;
-    const uint32_t wstride = segs[k].wstride ? segs[k].wstride : nk;
-    uint32_t* ki = w.key_in.as<uint32_t>() + eoff;
-    uint32_t* ei = w.ent_in.as<uint32_t>() + eoff;
-    if (sw == 1)
-      k_msm_keys<1><<<nb, 256, 0, st>>>(segs[k].scalars, p, nk, nseg > 1 ? kbase : 0u, wstride, segs[k].ioff, ki, ei);
-    else
-      k_msm_keys<4><<<nb, 256, 0, st>>>(segs[k].scalars, p, nk, 0u, nk, 0u, ki, ei);
-    ZK_LAUNCH_CHECK();
-    eoff += (size_t)nk * p.nwin;
-  }
-  if (M)
-    sort_pairs_u32(w.sort_tmp.p, tmp_bytes, w.key_in.as<uint32_t>(), w.key.as<uint32_t>(), w.ent_in.as<uint32_t>(),
-                   w.ent.as<uint32_t>(), M, end_bit, st);
-  k_msm_offsets<<<ceil_div(M + 1, 256), 256, 0, st>>>(w.key.as<uint32_t>(), (uint32_t)M, p.G, w.off.as<uint32_t>(),
-                                                      w.nbig.as<uint32_t>());
-  ZK_LAUNCH_CHECK();
+  // group the (point, window) entries by bucket: stable counting sort (group.hip)
+  msm_group(w, segs, nseg, sw, st);
   if (pf) pf->end(st, ph);
-  }
   // The number of non-zero digits M' <= M is known on device only: the T
   // accumulate threads split it evenly there (chunk_len), no host sync.
   if (M) {
@@ -1166,11 +1157,13 @@ static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hip
       k_msm_accum_pair<<<ceil_div(2 * (size_t)p.T, 128), 128, 0, st>>>(sb, p.segshift, w.ent.as<uint32_t>(),
                                                                         w.key.as<uint32_t>(), w.off.as<uint32_t>(),
                                                                         p.G, p.T, w.buckets.as<X>(),
-                                                                        w.partials.as<X>());
+                                                                        w.partials.as<X>(), w.nbig.as<uint32_t>(),
+                                                                        w.fixlist.as<uint32_t>());
     else
       k_msm_accum<C><<<ceil_div(p.T, 128), 128, 0, st>>>(sb, p.segshift, w.ent.as<uint32_t>(), w.key.as<uint32_t>(),
                                                           w.off.as<uint32_t>(), p.G, p.T, w.buckets.as<X>(),
-                                                          w.partials.as<X>());
+                                                          w.partials.as<X>(), w.nbig.as<uint32_t>(),
+                                                          w.fixlist.as<uint32_t>(), g1_inwave(p));
     ZK_LAUNCH_CHECK();
     if (pf) pf->end(st, ph);
   }
@@ -1185,14 +1178,22 @@ static void msm_back_impl(MsmWork& w, hipStream_t st, int mode, const MsmWork* p
   const uint32_t n = p.n;
   (void)n;
   int ph = pf ? pf->begin(st, (w.tag + "msm_merge").c_str(), p.G) : -1;   // buckets split across chunks
-  // ctl (w.nbig, zeroed by the front's k_msm_offsets / grouping): [0]
-  // buckets left to the merge, [1] its grid barrier
+  // ctl (w.nbig, zeroed by the front's k_msm_offsets): [0] buckets left to
+  // the merge, [1] its grid barrier, [2] the G1 fixup list's length
   const bool by_boundary = p.G > p.T;
   const size_t fix_n = by_boundary ? p.T : p.G;
-  if constexpr (g2)
+  if constexpr (g2 && ZK_FIX_INWAVE_G2)
+    k_msm_fixup_list_pair<<<ceil_div(2 * (size_t)std::min(p.G, p.T), 128), 128, 0, st>>>(
+        w.off.as<uint32_t>(), p.G, p.T, p.fix_max, w.nbig.as<uint32_t>(), w.fixlist.as<uint32_t>(),
+        reinterpret_cast<G2X*>(w.buckets.p), reinterpret_cast<const G2X*>(w.partials.p));
+  else if constexpr (g2)
     k_msm_fixup_pair<<<ceil_div(2 * fix_n, 128), 128, 0, st>>>(
         w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T, p.fix_max, by_boundary, w.nbig.as<uint32_t>(),
         reinterpret_cast<G2X*>(w.buckets.p), reinterpret_cast<const G2X*>(w.partials.p));
+  else if (ZK_FIX_INWAVE && g1_inwave(p))
+    k_msm_fixup_list<C><<<ceil_div(std::min(p.G, p.T), 128), 128, 0, st>>>(
+        w.off.as<uint32_t>(), p.G, p.T, p.fix_max, w.nbig.as<uint32_t>(), w.fixlist.as<uint32_t>(), w.buckets.as<X>(),
+        w.partials.as<X>());
   else
     k_msm_fixup<C><<<ceil_div(fix_n, 128), 128, 0, st>>>(w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T,
                                                           p.fix_max, by_boundary, w.nbig.as<uint32_t>(),

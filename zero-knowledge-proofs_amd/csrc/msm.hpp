@@ -8,8 +8,9 @@
 //
 // Pipeline per MSM (one HIP stream; workspace reused across calls):
 //   1 keys     signed c-bit window digits -> one (bucket, point | sign) pair
-//              per (point, window)
-//   2 sort     rocPRIM radix sort of the pairs by bucket, then bucket offsets
+//              per (point, window), computed inside step 2's first pass
+//   2 group    stable LSD counting sort of the pairs by bucket (group.hip),
+//              then bucket offsets
 //   4 accum    the M non-zero digits split evenly over one full-occupancy
 //              round of threads, XYZZ += affine with run-length flush:
 //              load-balanced whatever the digit distribution
@@ -33,6 +34,22 @@
 #include "host_ec.hpp"
 
 namespace zk {
+
+// Bits [off, off + width) of a little-endian scalar of SW u64 words.
+template <int SW>
+__device__ __forceinline__ uint32_t scal_window(const uint64_t (&s)[SW], int off, int width) {
+  int wd = off >> 6, sh = off & 63;
+  uint64_t lo = 0;
+#pragma unroll
+  for (int k = 0; k < SW; k++)
+    if (k == wd) lo = s[k] >> sh;
+  if (sh + width > 64) {
+#pragma unroll
+    for (int k = 0; k < SW; k++)
+      if (k == wd + 1) lo |= s[k] << (64 - sh);
+  }
+  return (uint32_t)(lo & ((1ull << width) - 1));
+}
 
 struct G1 {
   using F = Fq;
@@ -90,13 +107,15 @@ struct MsmSeg {
 };
 
 MsmPlan msm_make_plan(uint32_t n, int bits, int sw, int force_c = 0);
-// Bucket grouping without a general radix sort (group.hip) for shared / batch
-// plans with 16-bit bucket ids and <= 4 windows (every prove MSM at c = 16):
-// fills w.key / w.ent grouped by bucket (any order inside a bucket) and w.off.
+// Bucket grouping (group.hip): the (point, window) entries of the segments'
+// scalars (sw u64 words each), sorted stably by bucket into w.key / w.ent,
+// w.off[g] = first entry of bucket g (g <= G), and the merge's control
+// words w.nbig zeroed.  Deterministic: the same inputs give the same bytes.
 struct MsmWork;
 struct MsmSeg;
-bool msm_group_ok(const MsmPlan& p, int sw);
-void msm_group(MsmWork& w, const MsmSeg* segs, int nseg, hipStream_t st);
+void msm_group(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hipStream_t st);
+// w.off[] from the sorted w.key[0, M) (and w.nbig zeroed)
+void msm_offsets(MsmWork& w, uint32_t M, hipStream_t st);
 // Window-shared plan: digit window w of point i uses the precomputed base
 // 2^(c w) P_i (msm_precompute_windows), so every window accumulates into
 // ONE set of 2^max(c-1, top) buckets -- the bucket reduction shrinks by the
@@ -106,9 +125,10 @@ MsmPlan msm_make_plan_shared(uint32_t n, int bits, int sw, int c);
 // Device workspace of one in-flight MSM.
 struct MsmWork {
   DevBuf off, ent, key, buckets, partials, partials2, rc, res;
-  DevBuf key_in, ent_in, sort_tmp;   // radix-sort input and scratch
-  DevBuf nbig;                       // merge control words (msm_back_impl)
-  DevBuf gcnt, gcnt_off;             // bucket grouping (group.hip): per-tile coarse-bin counts, their scan
+  DevBuf key_in, ent_in;             // grouping: the other half of its ping-pong
+  DevBuf nbig;                       // control words: merge count, its grid barrier, fixup list length
+  DevBuf fixlist;                    // G1: buckets the accumulate left to the fixup
+  DevBuf gcnt, gcnt_sums;            // grouping (group.hip): per-tile digit counts / their scan, chunk sums
   PinnedBuf host_res;
   MsmPlan plan{};
   Prof* prof = nullptr;  // optional live kernel timing

@@ -438,11 +438,22 @@ void pk_precompute_windows(zk_ctx* ctx, zk_pk_dev& pk) {
   const int PROVE_WIN_C = prove_win_c(ctx, pk), PROVE_WIN = (64 + PROVE_WIN_C - 1) / PROVE_WIN_C;
   hipStream_t st = ctx->stream;
   for (int slot = 0; slot < NUM_MSM; slot++) {
-    const size_t n = (size_t)pk.count[slot] + pk.extras[slot];
+    if (slot == MSM_IC) continue;   // windowed together with H (zk_pk_dev::ich_tot)
+    const size_t n = slot == MSM_H ? pk.ich_tot() : (size_t)pk.count[slot] + pk.extras[slot];
     const size_t asz = slot == MSM_B2 ? sizeof(G2A) : sizeof(G1A);
     DevBuf big;
     big.ensure(asz * std::max<size_t>(n * PROVE_WIN, 1));
-    if (n) ZK_HIP(hipMemcpyAsync(big.p, pk.bases[slot].p, asz * n, hipMemcpyDeviceToDevice, st));
+    if (slot == MSM_H) {   // [IC | H]
+      const size_t nic = (size_t)pk.count[MSM_IC] + pk.extras[MSM_IC], nh = n - nic;
+      if (nic) ZK_HIP(hipMemcpyAsync(big.p, pk.bases[MSM_IC].p, asz * nic, hipMemcpyDeviceToDevice, st));
+      if (nh)
+        ZK_HIP(hipMemcpyAsync(static_cast<char*>(big.p) + asz * nic, pk.bases[MSM_H].p, asz * nh,
+                              hipMemcpyDeviceToDevice, st));
+      ZK_HIP(hipStreamSynchronize(st));
+      pk.bases[MSM_IC].release();
+    } else if (n) {
+      ZK_HIP(hipMemcpyAsync(big.p, pk.bases[slot].p, asz * n, hipMemcpyDeviceToDevice, st));
+    }
     if (slot == MSM_B2) msm_precompute_windows<G2>(big.as<G2A>(), n, PROVE_WIN, PROVE_WIN_C, st);
     else msm_precompute_windows<G1>(big.as<G1A>(), n, PROVE_WIN, PROVE_WIN_C, st);
     ZK_HIP(hipStreamSynchronize(st));
@@ -554,11 +565,15 @@ static bool uses_dist_quotient(const zk_ctx* ctx, const zk_pk_dev* pk) {
   return ctx->dist_quotient != 0 && exchange_matches(ctx, pk);
 }
 
-// The G1 MSMs run as two batches (msm_launch_batch: one sort, accumulate,
-// merge and bucket reduction per batch, so the latency-bound tails cost one
-// tree depth per batch): A, B1 and IC need only z and start with the
-// witness; H follows the quotient.
-static const int G1_ABI[3] = {MSM_A, MSM_B1, MSM_IC};
+// The G1 MSMs run as two pipelines (msm_launch_batch: one sort, accumulate,
+// merge and bucket reduction each, so the latency-bound tails cost one tree
+// depth per pipeline): A and B1, a batch of two MSMs that need only z, start
+// with the witness; IC and H -- both terms of pi_C = IC + H_1 + s pi_A +
+// r B_1 (core:224-265), so ONE MSM over the bases [ic_g1 | h_g1] with the
+// scalars [lo64(z_i) | lo64(H_i)] -- follows the quotient.  One bucket set
+// for IC and H: a bucket reduction fewer per proof than IC in the first batch
+// and H alone.
+static const int G1_AB[2] = {MSM_A, MSM_B1};
 
 // h_given (virtual-rank tests): this shard's lo64(H_(shard + nshards d)) is
 // already on the device, with the witness-check flags of all ranks.
@@ -626,6 +641,21 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   // extras' scalars (1 for alpha_1 / beta_2 / beta_1, the u64 limbs of r or s)
   auto prep_scalars = [&](int slot, hipStream_t ss) {
     const uint32_t cnt = pk->count[slot], nex = pk->extras[slot];
+    if (slot == MSM_H) {   // the IC + H MSM: [lo64(z_i) of IC's variables | lo64(H_i)]
+      const uint32_t nic = pk->count[MSM_IC];
+      ctx->scal[MSM_H].ensure(sizeof(uint64_t) * std::max<uint32_t>(pk->ich_tot(), 1));
+      if (nic) {
+        k_gather_lo64<<<ceil_div(nic, 256), 256, 0, ss>>>(d_z, 4, pk->idx[MSM_IC].as<uint32_t>(), 1u, nic,
+                                                          ctx->scal[MSM_H].as<uint64_t>());
+        ZK_LAUNCH_CHECK();
+      }
+      if (cnt) {
+        k_gather_lo64<<<ceil_div(cnt, 256), 256, 0, ss>>>(h_src, 1, pk->idx[MSM_H].as<uint32_t>(), h_div, cnt,
+                                                          ctx->scal[MSM_H].as<uint64_t>() + nic);
+        ZK_LAUNCH_CHECK();
+      }
+      return;
+    }
     ctx->scal[slot].ensure(sizeof(uint64_t) * std::max<uint32_t>(cnt + nex, 1));
     if (cnt) {
       const uint64_t* src = slot == MSM_H ? h_src : d_z;
@@ -691,17 +721,17 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       }
     }
     {
-      Range range("msm_g1_a_b1_ic_part");
-      MsmSeg segs[3];
-      for (int i = 0; i < 3; i++) {
-        const int sl = G1_ABI[i];
+      Range range("msm_g1_a_b1_part");
+      MsmSeg segs[2];
+      for (int i = 0; i < 2; i++) {
+        const int sl = G1_AB[i];
         const uint32_t lo = pk->pcut[part][sl], hi = pk->pcut[part + 1][sl];
         prep_range(sl, lo, hi, last, gsa);
         segs[i] = seg_range(sl, lo, last ? hi + pk->extras[sl] : hi);
       }
       MsmWork& w = last ? ctx->msm[MSM_A] : ctx->part_abi[part];
-      w.tag = serial ? (last ? "ABI/" : "ABIp/") : "";
-      msm_batch_front<G1>(w, segs, 3, 64, pk->win_c, gsa);
+      w.tag = serial ? (last ? "AB/" : "ABp/") : "";
+      msm_batch_front<G1>(w, segs, 2, 64, pk->win_c, gsa);
       msm_batch_back<G1>(w, gsa, mode, part ? &ctx->part_abi[part - 1] : nullptr);
       if (last) {
         msm_download<G1>(w, gsa);
@@ -711,12 +741,12 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   };
   static const char* const tags[NUM_MSM] = {"A/", "B2/", "B1/", "IC/", "H/"};
   auto launch_batch = [&](const int* slots, int k, const char* tag, hipStream_t gs) {
-    Range range(k == 1 ? "msm_g1_h" : "msm_g1_a_b1_ic");
+    Range range(k == 1 ? "msm_g1_ic_h" : "msm_g1_a_b1");
     MsmSeg segs[MSM_MAXSEG];
     for (int i = 0; i < k; i++) {
       prep_scalars(slots[i], gs);
-      segs[i] = MsmSeg{pk->bases[slots[i]].p, ctx->scal[slots[i]].as<uint64_t>(),
-                       pk->count[slots[i]] + pk->extras[slots[i]], pk->stride[slots[i]]};
+      const uint32_t np = slots[i] == MSM_H ? pk->ich_tot() : pk->count[slots[i]] + pk->extras[slots[i]];
+      segs[i] = MsmSeg{pk->bases[slots[i]].p, ctx->scal[slots[i]].as<uint64_t>(), np, pk->stride[slots[i]]};
     }
     MsmWork& w = ctx->msm[slots[0]];
     w.tag = serial ? tag : "";
@@ -738,7 +768,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       ZK_HIP(hipEventRecord(ctx->ev_done[MSM_B2], s_g2));
     }
     if (!serial) ZK_HIP(hipStreamWaitEvent(s_abi, ctx->ev_scal, 0));
-    launch_batch(G1_ABI, 3, "ABI/", s_abi);
+    launch_batch(G1_AB, 2, "AB/", s_abi);
   };
   // the quotient, then H on the main stream
   auto run_quotient = [&]() {
@@ -796,9 +826,9 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
   {
     const int h_slot[1] = {MSM_H};
-    launch_batch(h_slot, 1, "H/", st);
+    launch_batch(h_slot, 1, "ICH/", st);
   }
-  const int waits[3] = {MSM_B2, MSM_A, MSM_H};   // MSM_A: the A+B1+IC batch
+  const int waits[3] = {MSM_B2, MSM_A, MSM_H};   // MSM_A: the A+B1 batch, MSM_H: IC + H
   if (ph_span >= 0) {
     for (int sl : waits) ZK_HIP(hipStreamWaitEvent(st, ctx->ev_done[sl], 0));
     ctx->prof.end(st, ph_span);
@@ -832,10 +862,10 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       } else if (slot == MSM_A) {
         p.A = msm_finish_seg<G1>(ctx->msm[slot], 0);
         p.B1 = msm_finish_seg<G1>(ctx->msm[slot], 1);
-        p.IC = msm_finish_seg<G1>(ctx->msm[slot], 2);
         ab_done = true;
       } else {
-        p.H = msm_finish_seg<G1>(ctx->msm[slot], 0);
+        p.IC = msm_finish_seg<G1>(ctx->msm[slot], 0);   // IC + H_1
+        p.H = host::inf<host::Fq>();
       }
       done[wi] = progressed = true;
       left--;

@@ -77,10 +77,15 @@ int zk_test_pk_bases(zk_ctx* ctx, const zk_pk_dev* pk, int slot, int window, uin
   ZK_TGUARD(ctx, {
     const bool g2 = slot == MSM_B2;
     const size_t asz = g2 ? sizeof(G2A) : sizeof(G1A);
-    const size_t step = pk->stride[slot] ? pk->stride[slot] : asz;
-    const char* base = static_cast<const char*>(pk->bases[slot].p) + (size_t)window * tot * step;
+    // IC and H share one window buffer (bases[MSM_H]: each window [IC | H])
+    const bool ich = slot == MSM_IC || slot == MSM_H;
+    const int bslot = ich ? MSM_H : slot;
+    const size_t step = pk->stride[bslot] ? pk->stride[bslot] : asz;
+    const size_t wtot = ich ? pk->ich_tot() : tot;
+    const size_t skip = slot == MSM_H ? (size_t)pk->count[MSM_IC] + pk->extras[MSM_IC] : 0;
+    const char* base = static_cast<const char*>(pk->bases[bslot].p) + ((size_t)window * wtot + skip) * step;
     if (cnt) ZK_HIP(hipMemcpyAsync(idx_out, pk->idx[slot].p, sizeof(uint32_t) * cnt, hipMemcpyDeviceToHost, ctx->stream));
-    bases_to_abi_host(g2, base, pk->stride[slot], tot, words_out, ctx->stream);
+    bases_to_abi_host(g2, base, pk->stride[bslot], tot, words_out, ctx->stream);
     ZK_HIP(hipStreamSynchronize(ctx->stream));
     return ZK_OK;
   })

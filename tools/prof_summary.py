@@ -156,7 +156,7 @@ def calib(fetch_db, write_db, out, log_path):
 
 def pmc_prove(fetch_db, write_db, out, factor):
     """Per-dispatch FETCH/WRITE of a serial prove run; the accumulate
-    dispatches are split by their place in the prove (B2 G2, ABI batch, H)."""
+    dispatches are split by their place in the prove (B2 G2, the A+B1 batch, IC+H)."""
     fd, wd = dispatches(fetch_db, "FETCH_SIZE"), dispatches(write_db, "WRITE_SIZE")
     agg = {}
     for (_, k, fv), (_, k2, wv) in zip(fd, wd):
@@ -175,12 +175,14 @@ def pmc_prove(fetch_db, write_db, out, factor):
                    "profiles/r02_fetch_calibration.json); traffic_guide_2x = the guide's streaming correction",
            "kernels": kernels}
     if acc:
-        cut = max(f for f, _ in acc) / 2   # the A+B1+IC batch launch vs the H launch of each prove
+        # round 6: the IC+H launch (4n points) vs the A+B1 batch launch (2n)
+        # of each prove (rounds 1-5: the A+B1+IC batch vs H)
+        cut = max(f for f, _ in acc) / 1.5
         big = [a for a in acc if a[0] > cut]
         small = [a for a in acc if a[0] <= cut]
         per = lambda L: int(sum(factor * f + w for f, w in L) / len(L)) if L else None
-        res["msm_accum_g1_abi_bytes_per_launch"] = per(big)
-        res["msm_accum_g1_h_bytes_per_launch"] = per(small)
+        res["msm_accum_g1_ich_bytes_per_launch"] = per(big)
+        res["msm_accum_g1_ab_bytes_per_launch"] = per(small)
         res["msm_accum_g1_bytes_per_launch"] = per(acc)
     json.dump(res, open(out, "w"), indent=1)
     for k, v in res.items():

@@ -196,52 +196,6 @@ ZK_DI XYZZ<F> xyzz_add_ilp(const XYZZ<F>& p, const XYZZ<F>& q) {
   return xyzz_add_impl<F, false>(p, q);
 }
 
-// p + q with q's coordinates loaded from memory right before each use (and
-// reloaded for the second use) by ld(k), k = 0 X, 1 Y, 2 ZZ, 3 ZZZ, so the
-// add needs about the mixed add's registers: for the end of the bucket
-// accumulates, which run at 3 (G1) / 2 (G2 lane pairs) waves per SIMD.  The
-// doubling case (p == q) is not handled here: *dbl is set and the result is
-// meaningless (the caller leaves that bucket to the fixup).
-template <class F, class LD>
-ZK_DI XYZZ<F> xyzz_add_mem(const XYZZ<F>& p, LD ld, bool* dbl) {
-  *dbl = false;
-  if (f_is_zero(ld(2))) return p;
-  if (xyzz_is_inf(p)) return XYZZ<F>{ld(0), ld(1), ld(2), ld(3)};
-  F U1 = f_mul(p.X, ld(2));
-  ZK_SB();
-  F P = f_sub(f_mul(ld(0), p.ZZ), U1);
-  ZK_SB();
-  F S1 = f_mul(p.Y, ld(3));
-  ZK_SB();
-  F R = f_sub(f_mul(ld(1), p.ZZZ), S1);
-  ZK_SB();
-  XYZZ<F> r;
-  if (f_is_zero(P)) {
-    *dbl = f_is_zero(R);
-    xyzz_set_inf(r);   // p = -q
-    return r;
-  }
-  F PP = f_sqr(P);
-  ZK_SB();
-  r.ZZ = f_mul(p.ZZ, ld(2));
-  ZK_SB();
-  r.ZZ = f_mul(r.ZZ, PP);
-  ZK_SB();
-  F PPP = f_mul(P, PP);
-  ZK_SB();
-  r.ZZZ = f_mul(p.ZZZ, ld(3));
-  ZK_SB();
-  r.ZZZ = f_mul(r.ZZZ, PPP);
-  ZK_SB();
-  F Q = f_mul(U1, PP);
-  ZK_SB();
-  r.X = f_sub(f_sub(f_sqr(R), PPP), f_add(Q, Q));
-  ZK_SB();
-  r.Y = f_mul_sub(R, f_sub(Q, r.X), S1, PPP);
-  ZK_SB();
-  return r;
-}
-
 // ---- lane-quad cooperative add (latency-bound reductions) --------------
 // In the bucket-reduction trees a few hundred sums run at once, one or two
 // waves per SIMD, so an add costs its full instruction latency (~14 products

@@ -358,12 +358,12 @@ __global__ void __launch_bounds__(GS_THREADS) k_gs_scatter(GsArgs a, uint32_t sh
 }
 
 // off[g] = first sorted position with key >= g, for g in [0, G].
-// ctl (MsmWork::nbig): the merge's and the fixup list's control words,
-// zeroed here so that no memset launch is needed.
+// ctl (MsmWork::nbig): the merge's control words, zeroed here so that no
+// memset launch is needed.
 __global__ void __launch_bounds__(256) k_msm_offsets(const uint32_t* __restrict__ key, uint32_t M, uint32_t G,
                                                      uint32_t* __restrict__ off, uint32_t* __restrict__ ctl) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < 3) ctl[i] = 0;
+  if (i < 2) ctl[i] = 0;
   if (i > M) return;
   const uint32_t lo = i ? min(key[i - 1], G) + 1 : 0;     // keys in (key[i-1], key[i]] start at i
   const uint32_t hi = i < M ? min(key[i], G) : G;
@@ -371,7 +371,7 @@ __global__ void __launch_bounds__(256) k_msm_offsets(const uint32_t* __restrict_
 }
 
 void msm_offsets(MsmWork& w, uint32_t M, hipStream_t st) {
-  w.nbig.ensure(3 * sizeof(uint32_t));
+  w.nbig.ensure(2 * sizeof(uint32_t));
   k_msm_offsets<<<ceil_div((uint64_t)M + 1, 256), 256, 0, st>>>(w.key.as<uint32_t>(), M, w.plan.G,
                                                                  w.off.as<uint32_t>(), w.nbig.as<uint32_t>());
   ZK_LAUNCH_CHECK();

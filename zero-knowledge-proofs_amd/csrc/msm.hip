@@ -130,15 +130,6 @@ __device__ __forceinline__ uint32_t chunk_len(uint32_t M, uint32_t T) {
 // XCD (~6 MB) outgrow its 4 MB L2: each line came back from the fabric up to
 // 32 times; now at most 128 B / (4 B x ENTQ) = 2.  Reads may run ENTQ - 1
 // entries past the chunk (the arrays carry that slack).
-// G1: complete the buckets split over two chunks of one wave at the end of
-// the accumulate and list the rest for the fixup (k_msm_fixup_list);
-// ZK_FIX_INWAVE=0: A/B build with the per-bucket fixup of round 5
-#ifndef ZK_FIX_INWAVE
-#define ZK_FIX_INWAVE 1
-#endif
-#ifndef ZK_FIX_INWAVE_G2
-#define ZK_FIX_INWAVE_G2 1
-#endif
 constexpr uint32_t ENTQ = 16;
 constexpr uint32_t ENTQ_LDS_WORDS = 2 * ENTQ * 64;   // per wave
 struct EntQ {
@@ -212,9 +203,7 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_G1_ATTR k_msm_accum(SegBases<typ
                                                    const uint32_t* __restrict__ key,
                                                    const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
                                                    typename C::X* __restrict__ buckets,
-                                                   typename C::X* __restrict__ partials,
-                                                   uint32_t* __restrict__ ctl, uint32_t* __restrict__ fixlist,
-                                                   uint32_t inwave) {
+                                                   typename C::X* __restrict__ partials) {
   using X = typename C::X;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t M = off[G];  // grouped entries (known on device only)
@@ -249,36 +238,6 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_G1_ATTR k_msm_accum(SegBases<typ
   if (head) st_vec(&partials[2 * (size_t)t], acc);
   else if (tail) st_vec(&partials[2 * (size_t)t + 1], acc);
   else st_vec(&buckets[cur], acc);
-  if (ZK_FIX_INWAVE && inwave) {
-    // Buckets split over chunks t and t + 1 of the same wave (the common
-    // case for a batch: a bucket holds about one chunk's worth of entries)
-    // are completed here: the next lane's head piece is in memory (its own
-    // flush above), one add with that operand from memory.  Every other
-    // bucket that this chunk begins and a later one continues goes on the
-    // fixup list (ctl[2]), so the fixup touches only those.  Single G1 MSMs
-    // (H: buckets over ~4-6 chunks, so hardly any pair) keep the per-bucket
-    // fixup (inwave = 0): there the list only added a dependent load.
-    const uint32_t lane = threadIdx.x & 63;
-    const bool opens = tail && !head;   // this chunk holds the bucket's first entry
-    bool pair = opens && lane != 63 && off[cur + 1] <= end + K;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the wave's flushes, before the neighbours read them
-    bool listed = opens && !pair;
-    if (pair) {
-      bool dbl;
-      const Fq* q = reinterpret_cast<const Fq*>(&partials[2 * (size_t)t + 2]);
-      const X sum = xyzz_add_mem(acc, [&](int k) { return ld_vec(q + k); }, &dbl);
-      if (dbl) listed = true;   // p == q: the fixup's add doubles
-      else st_vec(&buckets[cur], sum);
-    }
-    const uint64_t lm = __ballot(listed);
-    if (lm) {
-      const uint32_t leader = (uint32_t)__ffsll((long long)lm) - 1;
-      uint32_t base = 0;
-      if (lane == leader) base = atomicAdd(&ctl[2], (uint32_t)__popcll(lm));
-      base = __shfl(base, (int)leader);
-      if (listed) fixlist[base + __popcll(lm & ((1ull << lane) - 1))] = cur;
-    }
-  }
 }
 
 // G2 accumulate over lane pairs (Fq2h, ff.hpp): chunk t is owned by lanes
@@ -297,9 +256,7 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_G2_ATTR k_msm_accum_pair(SegBase
                                                                       const uint32_t* __restrict__ key,
                                                                       const uint32_t* __restrict__ off, uint32_t G,
                                                                       uint32_t T, G2X* __restrict__ buckets,
-                                                                      G2X* __restrict__ partials,
-                                                                      uint32_t* __restrict__ ctl,
-                                                                      uint32_t* __restrict__ fixlist) {
+                                                                      G2X* __restrict__ partials) {
   const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
   const uint32_t h = pair_half();
   const uint32_t M = off[G];
@@ -334,32 +291,6 @@ __global__ void __launch_bounds__(128) ZK_ACCUM_G2_ATTR k_msm_accum_pair(SegBase
   if (head) st_pair(&partials[2 * (size_t)t], acc);
   else if (tail) st_pair(&partials[2 * (size_t)t + 1], acc);
   else st_pair(&buckets[cur], acc);
-  if constexpr (ZK_FIX_INWAVE_G2) {
-    // as k_msm_accum: the buckets split over two chunks of one wave (32 lane
-    // pairs) are completed here, the others listed for the fixup (by the
-    // pair's even lane); every branch below is pair-uniform
-    const uint32_t pl = (threadIdx.x & 63) >> 1;
-    const bool opens = tail && !head;
-    bool pair = opens && pl != 31 && off[cur + 1] <= end + K;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    bool listed = opens && !pair;
-    if (pair) {
-      bool dbl;
-      const Fq* q = reinterpret_cast<const Fq*>(&partials[2 * (size_t)t + 2]) + h;
-      const XYZZ<Fq2h> sum = xyzz_add_mem(acc, [&](int k) { return Fq2h{ld_vec(q + 2 * k)}; }, &dbl);
-      if (dbl) listed = true;
-      else st_pair(&buckets[cur], sum);
-    }
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t lm = __ballot(listed && h == 0);
-    if (lm) {
-      const uint32_t leader = (uint32_t)__ffsll((long long)lm) - 1;
-      uint32_t base = 0;
-      if (lane == leader) base = atomicAdd(&ctl[2], (uint32_t)__popcll(lm));
-      base = __shfl(base, (int)leader);
-      if (listed && h == 0) fixlist[base + __popcll(lm & ((1ull << lane) - 1))] = cur;
-    }
-  }
 }
 
 // Buckets whose entries span several accumulate chunks.  A bucket over
@@ -446,32 +377,6 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
   if (t0 == t1) return;
   if (t1 - t0 + 1 > fix_max) {   // left to the merge levels, which skip themselves when none exist
     atomicAdd(nbig, 1u);
-    return;
-  }
-  X acc = ld_vec(&partials[2 * (size_t)t0 + 1]);
-  for (uint32_t t = t0 + 1; t <= t1; t++) acc = tail_add(acc, ld_vec(&partials[2 * (size_t)t]));
-  st_vec(&buckets[g], acc);
-}
-
-// The fixup of the listed buckets (ZK_FIX_INWAVE): ctl[2] buckets that the
-// accumulate could not complete in its own wave, each summed serially from
-// its chunk pieces by one thread (the list's order does not matter: each
-// thread writes its own bucket, in chunk order), buckets over more than
-// fix_max chunks left to the merge.
-template <class C>
-__global__ void __launch_bounds__(128) k_msm_fixup_list(const uint32_t* __restrict__ off, uint32_t G, uint32_t T,
-                                                        uint32_t fix_max, uint32_t* __restrict__ ctl,
-                                                        const uint32_t* __restrict__ list,
-                                                        typename C::X* __restrict__ buckets,
-                                                        const typename C::X* __restrict__ partials) {
-  using X = typename C::X;
-  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= ctl[2]) return;
-  const uint32_t K = chunk_len(off[G], T);
-  const uint32_t g = list[u];
-  const uint32_t t0 = off[g] / K, t1 = (off[g + 1] - 1) / K;
-  if (t1 - t0 + 1 > fix_max) {   // left to the merge levels
-    atomicAdd(&ctl[0], 1u);
     return;
   }
   X acc = ld_vec(&partials[2 * (size_t)t0 + 1]);
@@ -941,27 +846,6 @@ __global__ void __launch_bounds__(128) k_msm_fixup_pair(const uint32_t* __restri
   st_pair(&buckets[g], acc);
 }
 
-// The G2 listed-bucket fixup (ZK_FIX_INWAVE_G2) on lane pairs.
-__global__ void __launch_bounds__(128) k_msm_fixup_list_pair(const uint32_t* __restrict__ off, uint32_t G,
-                                                             uint32_t T, uint32_t fix_max, uint32_t* __restrict__ ctl,
-                                                             const uint32_t* __restrict__ list,
-                                                             G2X* __restrict__ buckets,
-                                                             const G2X* __restrict__ partials) {
-  const uint32_t u = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;   // pair-uniform from here on
-  if (u >= ctl[2]) return;
-  const uint32_t K = chunk_len(off[G], T);
-  const uint32_t g = list[u];
-  const uint32_t t0 = off[g] / K, t1 = (off[g + 1] - 1) / K;
-  if (t1 - t0 + 1 > fix_max) {
-    if (!pair_half()) atomicAdd(&ctl[0], 1u);
-    return;
-  }
-  XYZZ<Fq2h> acc = ld_pair(&partials[2 * (size_t)t0 + 1]);
-#pragma unroll 1
-  for (uint32_t t = t0 + 1; t <= t1; t++) acc = tail_add(acc, ld_pair(&partials[2 * (size_t)t]));
-  st_pair(&buckets[g], acc);
-}
-
 // Two parts of one split MSM (msm_batch_back COMBINE): bucket g = this
 // part's bucket + the earlier part's, each only where its part had entries,
 // written for EVERY bucket (infinity where both are empty), so the reduction
@@ -1099,10 +983,6 @@ static void msm_split_sums(MsmPlan& p, uint32_t target, uint32_t lanes) {
   }
 }
 
-// G1 plans whose accumulate completes two-chunk buckets in its waves and
-// lists the rest (ZK_FIX_INWAVE): batches (the A+B1+IC MSMs)
-static inline uint32_t g1_inwave(const MsmPlan& p) { return ZK_FIX_INWAVE && p.nseg > 1 ? 1u : 0u; }
-
 // Buckets spread over at most this many accumulate chunks are summed by the
 // serial fixup; larger ones go through the log-depth merge.
 constexpr uint32_t MSM_FIX_MAX = 8;
@@ -1132,7 +1012,6 @@ static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hip
   // (profiles/r05_ab_qtail_slowbox.txt)
   if (g2 ? ZK_SPLIT_G2 : ZK_SPLIT_G1) msm_split_sums(p, rowcol_waves<C>(), g2 ? 32u : 64u);
   w.partials.ensure(sizeof(X) * 2 * (size_t)p.T);
-  w.fixlist.ensure(sizeof(uint32_t) * std::max<uint32_t>(std::min(p.G, p.T), 1));
   w.partials2.ensure(sizeof(X) * ((size_t)p.T / 2 + 2));
   w.rc.ensure(sizeof(X) * p.nrc);
   w.res.ensure(sizeof(X) * p.nq);
@@ -1157,13 +1036,11 @@ static void msm_front_impl(MsmWork& w, const MsmSeg* segs, int nseg, int sw, hip
       k_msm_accum_pair<<<ceil_div(2 * (size_t)p.T, 128), 128, 0, st>>>(sb, p.segshift, w.ent.as<uint32_t>(),
                                                                         w.key.as<uint32_t>(), w.off.as<uint32_t>(),
                                                                         p.G, p.T, w.buckets.as<X>(),
-                                                                        w.partials.as<X>(), w.nbig.as<uint32_t>(),
-                                                                        w.fixlist.as<uint32_t>());
+                                                                        w.partials.as<X>());
     else
       k_msm_accum<C><<<ceil_div(p.T, 128), 128, 0, st>>>(sb, p.segshift, w.ent.as<uint32_t>(), w.key.as<uint32_t>(),
                                                           w.off.as<uint32_t>(), p.G, p.T, w.buckets.as<X>(),
-                                                          w.partials.as<X>(), w.nbig.as<uint32_t>(),
-                                                          w.fixlist.as<uint32_t>(), g1_inwave(p));
+                                                          w.partials.as<X>());
     ZK_LAUNCH_CHECK();
     if (pf) pf->end(st, ph);
   }
@@ -1179,21 +1056,13 @@ static void msm_back_impl(MsmWork& w, hipStream_t st, int mode, const MsmWork* p
   (void)n;
   int ph = pf ? pf->begin(st, (w.tag + "msm_merge").c_str(), p.G) : -1;   // buckets split across chunks
   // ctl (w.nbig, zeroed by the front's k_msm_offsets): [0] buckets left to
-  // the merge, [1] its grid barrier, [2] the G1 fixup list's length
+  // the merge, [1] its grid barrier
   const bool by_boundary = p.G > p.T;
   const size_t fix_n = by_boundary ? p.T : p.G;
-  if constexpr (g2 && ZK_FIX_INWAVE_G2)
-    k_msm_fixup_list_pair<<<ceil_div(2 * (size_t)std::min(p.G, p.T), 128), 128, 0, st>>>(
-        w.off.as<uint32_t>(), p.G, p.T, p.fix_max, w.nbig.as<uint32_t>(), w.fixlist.as<uint32_t>(),
-        reinterpret_cast<G2X*>(w.buckets.p), reinterpret_cast<const G2X*>(w.partials.p));
-  else if constexpr (g2)
+  if constexpr (g2)
     k_msm_fixup_pair<<<ceil_div(2 * fix_n, 128), 128, 0, st>>>(
         w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T, p.fix_max, by_boundary, w.nbig.as<uint32_t>(),
         reinterpret_cast<G2X*>(w.buckets.p), reinterpret_cast<const G2X*>(w.partials.p));
-  else if (ZK_FIX_INWAVE && g1_inwave(p))
-    k_msm_fixup_list<C><<<ceil_div(std::min(p.G, p.T), 128), 128, 0, st>>>(
-        w.off.as<uint32_t>(), p.G, p.T, p.fix_max, w.nbig.as<uint32_t>(), w.fixlist.as<uint32_t>(), w.buckets.as<X>(),
-        w.partials.as<X>());
   else
     k_msm_fixup<C><<<ceil_div(fix_n, 128), 128, 0, st>>>(w.key.as<uint32_t>(), w.off.as<uint32_t>(), p.G, p.T,
                                                           p.fix_max, by_boundary, w.nbig.as<uint32_t>(),

@@ -126,8 +126,7 @@ MsmPlan msm_make_plan_shared(uint32_t n, int bits, int sw, int c);
 struct MsmWork {
   DevBuf off, ent, key, buckets, partials, partials2, rc, res;
   DevBuf key_in, ent_in;             // grouping: the other half of its ping-pong
-  DevBuf nbig;                       // control words: merge count, its grid barrier, fixup list length
-  DevBuf fixlist;                    // G1: buckets the accumulate left to the fixup
+  DevBuf nbig;                       // control words: merge count, its grid barrier
   DevBuf gcnt, gcnt_sums;            // grouping (group.hip): per-tile digit counts / their scan, chunk sums
   PinnedBuf host_res;
   MsmPlan plan{};

@@ -168,7 +168,7 @@ def pmc_prove(fetch_db, write_db, out, factor):
     kernels = {k: {"dispatches": n, "fetch_bytes": int(fb / n), "write_bytes": int(wb / n),
                    "traffic_guide_2x": int((2 * fb + wb) / n), "traffic_calibrated": int((factor * fb + wb) / n)}
                for k, (n, fb, wb) in sorted(agg.items())}
-    acc = [(fv * 1024, wv * 1024) for (_, k, fv), (_, _, wv) in zip(fd, wd) if "k_msm_accum" in k and "pair" not in k]
+    acc = [(fv * 1024, wv * 1024) for (_, k, fv), (_, _, wv) in zip(fd, wd) if short(k) == "k_msm_accum<G1>"]
     res = {"note": f"serial prove (zk_ctx_set_schedule 3); traffic_calibrated = {factor} x FETCH_SIZE + WRITE_SIZE "
                    "(FETCH factor from tools/gather_calib for the accumulate's gather shape -- 1.779 for 96-byte "
                    "points read at a 128-byte stride (k_gather<6,8>), 1.585 for packed 96-byte points -- "
@@ -211,7 +211,7 @@ def part(fetch_db, write_db, out, kind, calls, factor):
     res = {"kind": kind, "calls": calls, "fetch_factor": f, "kernels": kernels}
     if kind == "msm":
         acc = [(fv * 1024, wv * 1024) for (_, k, fv), (_, _, wv) in zip(fd, wd)
-               if "k_msm_accum" in k and "pair" not in k]
+               if short(k) == "k_msm_accum<G1>"]
         res["bytes_per_launch"] = int(sum(f * a + b for a, b in acc) / len(acc))
         per_call = [(fv * 1024, wv * 1024) for (_, k, fv), (_, _, wv) in zip(fd, wd)
                     if "k_msm" in k or "rocprim" in k]   # not the setup / base upload kernels

@@ -957,6 +957,16 @@ static uint32_t rowcol_waves() {
 #ifndef ZK_SPLIT_G2
 #define ZK_SPLIT_G2 0
 #endif
+// Partials keep >= ZK_SPLIT_MIN terms per lane: the prove plans' 256-term
+// rows and columns stay whole (4 per lane; their quantities then fold 128
+// terms instead of 256-512), the standalone plans' 512-1024-term sums split
+// to 256.  Round 6 (2 -> 4, profiles/r06_ab_split_min.txt): serial A+B1
+// bucket sum 0.298 -> 0.245 ms, overlapped prove median 8.626 -> 8.511 ms,
+// configs[1] MSM unchanged (3.27-3.29 ms); no split at all cost that MSM
+// 0.1 ms.
+#ifndef ZK_SPLIT_MIN
+#define ZK_SPLIT_MIN 4
+#endif
 static void msm_split_sums(MsmPlan& p, uint32_t target, uint32_t lanes) {
   auto recount = [&]() {
     uint32_t rc = 0;
@@ -975,7 +985,7 @@ static void msm_split_sums(MsmPlan& p, uint32_t target, uint32_t lanes) {
       if (rlen > blen) { blen = rlen; bw = (int)w; brow = true; }
       if (clen > blen) { blen = clen; bw = (int)w; brow = false; }
     }
-    if (bw < 0 || blen / 2 < 2 * lanes) break;
+    if (bw < 0 || blen / 2 < ZK_SPLIT_MIN * lanes) break;
     const uint32_t add = brow ? 1u << (p.kr[bw] + p.lsr[bw]) : 1u << (p.kc[bw] + p.lsc[bw]);
     if ((uint64_t)p.nrc + add > target) break;
     (brow ? p.lsr : p.lsc)[bw]++;

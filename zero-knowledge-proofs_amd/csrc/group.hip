@@ -56,7 +56,6 @@ constexpr uint32_t GS_WR = GS_IPT;                  // rounds of 64 entries per 
 #endif
 constexpr uint32_t GS_MAXRB = ZK_GS_RB;
 constexpr uint32_t GS_MAXNB = 1u << GS_MAXRB;
-constexpr int GS_MAXPASS = 3;
 constexpr uint32_t GS_SCAN_ITEMS = 8;               // scan: counters per thread
 constexpr uint32_t GS_SCAN_THREADS = 1024;
 constexpr uint32_t GS_SCAN_CHUNK = GS_SCAN_ITEMS * GS_SCAN_THREADS;

@@ -71,6 +71,7 @@ zk_ctx* zk_ctx_create(int device) {
     ZK_HIP(hipEventCreateWithFlags(&c->ev_scal, hipEventDisableTiming));
     ZK_HIP(hipEventCreateWithFlags(&c->ev_quot, hipEventDisableTiming));
     for (auto& e : c->ev_done) ZK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ZK_HIP(hipEventCreateWithFlags(&c->ev_ic, hipEventDisableTiming));
     return c.release();
   } catch (...) {
     return nullptr;
@@ -88,6 +89,7 @@ void zk_ctx_destroy(zk_ctx* ctx) {
   (void)hipEventDestroy(ctx->ev_scal);
   (void)hipEventDestroy(ctx->ev_quot);
   for (auto& e : ctx->ev_done) (void)hipEventDestroy(e);
+  (void)hipEventDestroy(ctx->ev_ic);
   delete ctx;
 }
 

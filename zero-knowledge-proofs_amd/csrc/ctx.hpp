@@ -39,6 +39,7 @@ struct zk_ctx {
   hipEvent_t ev_scal = nullptr;                 // witness checked (flags reset)
   hipEvent_t ev_quot = nullptr;                 // quotient done (ZK_OPT_EXCHANGE_FIRST)
   hipEvent_t ev_done[zk::NUM_MSM] = {};         // per-MSM completion (results downloaded)
+  hipEvent_t ev_ic = nullptr;                   // IC's scalars gathered (side stream)
   std::string err;
   zk::MsmWork msm[zk::NUM_MSM];
   // the G2 and A+B1+IC MSMs' workspaces for every part of a host witness

@@ -639,16 +639,23 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   const uint32_t h_div = (h_given || dist) ? pk->nshards : 1;
   // scalars of one MSM: lo64 of its variables (or H coefficients), then the
   // extras' scalars (1 for alpha_1 / beta_2 / beta_1, the u64 limbs of r or s)
+  // IC's scalars need only z: gathered ahead of the quotient on the A+B1
+  // stream (ev_ic), so that the IC+H grouping starts right after the quotient
+  bool ic_ready = false;
+  auto prep_ic = [&](hipStream_t ss) {
+    const uint32_t nic = pk->count[MSM_IC];
+    ctx->scal[MSM_H].ensure(sizeof(uint64_t) * std::max<uint32_t>(pk->ich_tot(), 1));
+    if (nic) {
+      k_gather_lo64<<<ceil_div(nic, 256), 256, 0, ss>>>(d_z, 4, pk->idx[MSM_IC].as<uint32_t>(), 1u, nic,
+                                                        ctx->scal[MSM_H].as<uint64_t>());
+      ZK_LAUNCH_CHECK();
+    }
+  };
   auto prep_scalars = [&](int slot, hipStream_t ss) {
     const uint32_t cnt = pk->count[slot], nex = pk->extras[slot];
     if (slot == MSM_H) {   // the IC + H MSM: [lo64(z_i) of IC's variables | lo64(H_i)]
       const uint32_t nic = pk->count[MSM_IC];
-      ctx->scal[MSM_H].ensure(sizeof(uint64_t) * std::max<uint32_t>(pk->ich_tot(), 1));
-      if (nic) {
-        k_gather_lo64<<<ceil_div(nic, 256), 256, 0, ss>>>(d_z, 4, pk->idx[MSM_IC].as<uint32_t>(), 1u, nic,
-                                                          ctx->scal[MSM_H].as<uint64_t>());
-        ZK_LAUNCH_CHECK();
-      }
+      if (!ic_ready) prep_ic(ss);
       if (cnt) {
         k_gather_lo64<<<ceil_div(cnt, 256), 256, 0, ss>>>(h_src, 1, pk->idx[MSM_H].as<uint32_t>(), h_div, cnt,
                                                           ctx->scal[MSM_H].as<uint64_t>() + nic);
@@ -768,6 +775,11 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       ZK_HIP(hipEventRecord(ctx->ev_done[MSM_B2], s_g2));
     }
     if (!serial) ZK_HIP(hipStreamWaitEvent(s_abi, ctx->ev_scal, 0));
+    if (!serial) {
+      prep_ic(s_abi);
+      ZK_HIP(hipEventRecord(ctx->ev_ic, s_abi));
+      ic_ready = true;
+    }
     launch_batch(G1_AB, 2, "AB/", s_abi);
   };
   // the quotient, then H on the main stream
@@ -826,6 +838,7 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   ZK_HIP(hipMemcpyAsync(ctx->flags_host.p, ctx->flags.p, 4, hipMemcpyDeviceToHost, st));
   {
     const int h_slot[1] = {MSM_H};
+    if (ic_ready) ZK_HIP(hipStreamWaitEvent(st, ctx->ev_ic, 0));
     launch_batch(h_slot, 1, "ICH/", st);
   }
   const int waits[3] = {MSM_B2, MSM_A, MSM_H};   // MSM_A: the A+B1 batch, MSM_H: IC + H

@@ -89,6 +89,10 @@ struct zk_pk_dev {
   // empty once the windows are built.
   int win = 1, win_c = 0;
   uint32_t ich_tot() const { return count[zk::MSM_IC] + extras[zk::MSM_IC] + count[zk::MSM_H] + extras[zk::MSM_H]; }
+  // idx[MSM_H][k] == k for every compacted H base (an unsharded key without
+  // identity H bases): the local quotient then writes lo64(H_i) straight
+  // into the IC+H scalar vector and no gather follows it
+  bool h_ident = false;
   // Bytes between consecutive bases of bases[slot]: 0 = packed (sizeof the
   // affine point), else padded to whole 128-B lines (msm_pad_bases).
   uint32_t stride[zk::NUM_MSM] = {};

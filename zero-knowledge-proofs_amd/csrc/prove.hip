@@ -219,6 +219,10 @@ static void upload_vector(zk_pk_dev& pk, int slot, const ABI* v, uint64_t lo, ui
     }
   const uint32_t cnt = (uint32_t)gidx.size();
   const uint32_t nex = (uint32_t)extras.size();
+  if (slot == MSM_H) {
+    pk.h_ident = true;
+    for (uint32_t k = 0; k < cnt; k++) pk.h_ident = pk.h_ident && gidx[k] == k;
+  }
   pk.count[slot] = cnt;
   pk.extras[slot] = nex;
   pk.bases[slot].ensure(sizeof(typename C::A) * std::max<uint64_t>(cnt + nex, 1));
@@ -477,7 +481,7 @@ struct Partial {
 };
 static_assert(sizeof(Partial) <= ZK_PARTIAL_BYTES, "partial size");
 
-static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipStream_t st) {
+static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipStream_t st, uint64_t* h_out) {
   const uint64_t n = pk->n;
   NttDomain& dom = ctx->domain(pk->log_n);
   ctx->qabc.ensure(sizeof(Fr) * 3 * n);
@@ -527,12 +531,11 @@ static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipS
   // natural order (the bit reversal is the first pass's tiled gather,
   // n^-1 g^-i fused into the last pass's store) into v[1], v[2] as scratch,
   // since beyond the MALL every gathered 32-B element was its own line/page
-  ctx->scal[MSM_H].ensure(sizeof(uint64_t) * n);
   ctx->tmp_scal.ensure(sizeof(uint64_t) * n);
   if (!large) {
     ntt_dif(v[0], dom, true, st, pf);
     ph = pf->begin(st, "quotient_misc", n);
-    k_h_final<<<ceil_div(n, 256), 256, 0, st>>>(v[0], domain_gipow(dom, st), pk->log_n, ctx->tmp_scal.as<uint64_t>());
+    k_h_final<<<ceil_div(n, 256), 256, 0, st>>>(v[0], domain_gipow(dom, st), pk->log_n, h_out);
     ZK_LAUNCH_CHECK();
     pf->end(st, ph);
     return;
@@ -545,7 +548,7 @@ static void quotient(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d_z, hipS
     ntt_natural(v[1], v[0], v[2], dom, true, st, pf, nullptr, domain_gipow(dom, st), nullptr);
   }
   ph = pf->begin(st, "quotient_misc", n);
-  k_h_lo64<<<ceil_div(n, 256), 256, 0, st>>>(h, n, ctx->tmp_scal.as<uint64_t>());
+  k_h_lo64<<<ceil_div(n, 256), 256, 0, st>>>(h, n, h_out);
   ZK_LAUNCH_CHECK();
   pf->end(st, ph);
 }
@@ -642,9 +645,12 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   // IC's scalars need only z: gathered ahead of the quotient on the A+B1
   // stream (ev_ic), so that the IC+H grouping starts right after the quotient
   bool ic_ready = false;
+  // the IC+H scalar vector, sized once before any stream writes it (IC's
+  // gather on the A+B1 stream, H's lo64 from the quotient when h_direct)
+  const uint32_t nic = pk->count[MSM_IC];
+  const bool h_direct = pk->h_ident && !dist && !h_given;
+  ctx->scal[MSM_H].ensure(sizeof(uint64_t) * std::max<uint64_t>({(uint64_t)pk->ich_tot(), (uint64_t)nic + pk->n, 1}));
   auto prep_ic = [&](hipStream_t ss) {
-    const uint32_t nic = pk->count[MSM_IC];
-    ctx->scal[MSM_H].ensure(sizeof(uint64_t) * std::max<uint32_t>(pk->ich_tot(), 1));
     if (nic) {
       k_gather_lo64<<<ceil_div(nic, 256), 256, 0, ss>>>(d_z, 4, pk->idx[MSM_IC].as<uint32_t>(), 1u, nic,
                                                         ctx->scal[MSM_H].as<uint64_t>());
@@ -654,9 +660,8 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
   auto prep_scalars = [&](int slot, hipStream_t ss) {
     const uint32_t cnt = pk->count[slot], nex = pk->extras[slot];
     if (slot == MSM_H) {   // the IC + H MSM: [lo64(z_i) of IC's variables | lo64(H_i)]
-      const uint32_t nic = pk->count[MSM_IC];
       if (!ic_ready) prep_ic(ss);
-      if (cnt) {
+      if (cnt && !h_direct) {
         k_gather_lo64<<<ceil_div(cnt, 256), 256, 0, ss>>>(h_src, 1, pk->idx[MSM_H].as<uint32_t>(), h_div, cnt,
                                                           ctx->scal[MSM_H].as<uint64_t>() + nic);
         ZK_LAUNCH_CHECK();
@@ -791,7 +796,10 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       h_src = ctx->tmp_scal.as<uint64_t>();
       dist_quotient(ctx, pk, d_z, *ctx->exch, ctx->dq, ctx->flags.as<uint32_t>(), ctx->tmp_scal.as<uint64_t>(), st);
     } else {
-      quotient(ctx, pk, d_z, st);   // (Az, Bz, Cz) -> lo64(H) in tmp_scal
+      // (Az, Bz, Cz) -> lo64(H): in place in the IC+H scalars, else in
+      // tmp_scal (sized here, before its pointer is taken)
+      ctx->tmp_scal.ensure(sizeof(uint64_t) * pk->n);
+      quotient(ctx, pk, d_z, st, h_direct ? ctx->scal[MSM_H].as<uint64_t>() + nic : ctx->tmp_scal.as<uint64_t>());
       h_src = ctx->tmp_scal.as<uint64_t>();
     }
   };

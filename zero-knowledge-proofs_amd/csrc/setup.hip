@@ -507,6 +507,10 @@ int setup_impl(zk_ctx* ctx, const zk_r1cs_csr* q, const zk_setup_params* P, uint
       }
     const uint32_t cnt = (uint32_t)loc.size();
     const size_t asz = g2 ? sizeof(G2A) : sizeof(G1A);
+    if (slot == MSM_H) {
+      d->h_ident = true;
+      for (uint32_t k = 0; k < cnt; k++) d->h_ident = d->h_ident && glob[k] == k;
+    }
     d->count[slot] = cnt;
     d->extras[slot] = nextra;
     d->bases[slot].ensure(asz * std::max<uint64_t>(cnt + nextra, 1));

@@ -826,6 +826,11 @@ static Partial prove_partial(zk_ctx* ctx, const zk_pk_dev* pk, const uint64_t* d
       if (!serial) {
         ZK_HIP(hipStreamWaitEvent(s_g2, ctx->ev_scal, 0));
         ZK_HIP(hipStreamWaitEvent(s_abi, ctx->ev_scal, 0));
+        if (k == HOST_PARTS - 1) {   // all of z is here: IC's scalars off the critical path too
+          prep_ic(s_abi);
+          ZK_HIP(hipEventRecord(ctx->ev_ic, s_abi));
+          ic_ready = true;
+        }
       }
       launch_part(k, s_g2, s_abi);
     }

@@ -1283,6 +1283,12 @@ def main():
                                      max(2, args.steps // 4), anc["msm_only"]["ms_per_step"], anc["proof_compressed"])
                 anc[f"shard{args.shard_scaling}_msm_only"] = sh
                 anc[f"msm_scaling_projected_{args.shard_scaling}"] = sh["msm_scaling_projected"]
+                if "same_plan_c16" in anc:
+                    # the same ratio at an equal window plan (c = 16 on both
+                    # sides): what sharding itself costs, without the one-GPU
+                    # anchor's c = 22 saving (3 windows instead of 4)
+                    anc[f"msm_scaling_projected_{args.shard_scaling}_same_plan"] = round(
+                        anc["same_plan_c16"]["msm_only"]["ms_per_step"] / sh["ms_per_step"], 3)
             extra["strong_scaling_anchor"] = anc
     if rank == 0:
         if world == 1:
